@@ -1,0 +1,149 @@
+/*
+ * vgposp.h — C-ABI of libvgposp.so, the MI355X (gfx950) hot path of DL-WG/VGPosp:
+ * GP kernel assembly -> fp64 Cholesky (+ fused inverse) -> GP log-marginal-likelihood / gradient
+ * -> greedy mutual-information sensor placement.
+ *
+ * The reference exposes this path as Python (TF1 graph + TFP + numpy).  Each entry point below
+ * names the reference interface it replaces (file:line under the reference checkout).  Bindings:
+ * vgposp_amd/_lib.py (ctypes); a maintainer-side ctypes stub for the reference is in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - Every array argument is a caller-owned DEVICE pointer (e.g. a torch tensor's data_ptr());
+ *     the library never allocates device memory.  Scratch is passed in as `ws`/`ws_bytes`, sized
+ *     by the matching *_workspace_bytes() query.
+ *   - Matrices are row-major fp64 with an explicit leading dimension (elements).  Batched
+ *     operands are `batch` matrices `stride` elements apart.
+ *   - `stream` is a hipStream_t (may be NULL = default stream).  Calls only enqueue work: no host
+ *     synchronisation happens inside the library, so device-side status (`info`) must be read by
+ *     the caller after synchronising.
+ *   - Return: 0 = enqueued; -i = argument i (1-based) invalid; VGPOSP_E_HIP = HIP runtime error;
+ *     VGPOSP_E_WS = workspace too small.  vgposp_last_error() returns a thread-local message.
+ *   - Device `info` (int32 per batch entry): 0 = success, k > 0 = the leading minor of order k
+ *     is not positive definite (LAPACK potrf convention).  The Python layer maps k > 0 to the
+ *     TF error "Cholesky decomposition was not successful".
+ *   - Stateless and re-entrant; concurrent calls on different streams with disjoint buffers are
+ *     safe.
+ */
+#ifndef VGPOSP_H_
+#define VGPOSP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VGPOSP_ABI_VERSION 1
+
+#define VGPOSP_E_HIP (-100)
+#define VGPOSP_E_WS (-101)
+
+/* PSD kernel families (tfp.positive_semidefinite_kernels). */
+#define VGPOSP_KERNEL_EQ 0       /* ExponentiatedQuadratic: 3D_sin_wave.py:158-159, main_tests.py:617 */
+#define VGPOSP_KERNEL_MATERN12 1 /* MaternOneHalf: gp_functions.py:160-163, main.py:94 */
+#define VGPOSP_KERNEL_MATERN32 2 /* MaternThreeHalves */
+#define VGPOSP_KERNEL_MATERN52 3 /* MaternFiveHalves: main_architecture_2_sampledistribution.py:211 */
+
+/* Output triangle selectors. */
+#define VGPOSP_FULL 0
+#define VGPOSP_LOWER 1
+
+int vgposp_abi_version(void);
+const char* vgposp_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Kernel assembly.  Replaces `kernel.matrix(x1, x2)` of the TFP PSD kernels built by
+ * gp_functions.create_cov_kernel (gp_functions.py:160-163) and consumed by tfd.GaussianProcess
+ * (gp_functions.py:166-172), GPRM (:283-297) and the VGP (variational_Gaussian_process_example.py
+ * :55-89):
+ *     K[b][i][j] = exp(2*log(amp[b]) + log k(|X1_i - X2_j| / ls[b])) + (i==j ? diag_shift[b] : 0)
+ * X1: n1 x d, X2: n2 x d (row-major, d <= 8).  amp, ls: [batch] device arrays.  diag_shift:
+ * [batch] device array or NULL (added on i == j, used for noise + jitter of a symmetric K).
+ * uplo = VGPOSP_LOWER writes only j <= i (the upper triangle is left untouched).
+ * --------------------------------------------------------------------------------------------- */
+int vgposp_kernel_matrix(int kind, const double* X1, int64_t n1, const double* X2, int64_t n2,
+                         int d, const double* amp, const double* ls, const double* diag_shift,
+                         int batch, int uplo, double* K, int64_t ldk, int64_t stride_k,
+                         void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * fp64 GEMM on MFMA (v_mfma_f64_16x16x4f64):  C = alpha * op(A) * op(B) + beta * C
+ * op(A) = A (m x k, transa=0) or A^T (A stored k x m, transa=1);
+ * op(B) = B (k x n, transb=0) or B^T (B stored n x k, transb=1).
+ * uplo_c = VGPOSP_LOWER updates only the lower triangle of C (j <= i).  tri_a / tri_b = 1 treat
+ * the STORED A / B as lower triangular (entries above their diagonal read as 0).
+ * The building block of the Cholesky trailing update / TRMM / C^-1 formation below.
+ * --------------------------------------------------------------------------------------------- */
+int vgposp_gemm(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Blocked right-looking Cholesky, lower, in place.  Replaces tf.linalg.cholesky inside
+ * tfd.GaussianProcess.log_prob / GPRM / VGP (gp_functions.py:166-172, main.py:105,
+ * 3D_sin_wave.py:172) and is the O(N^3) core of the dense greedy placement.
+ *   invert = 0: lower triangle of A <- L with A = L L^T.
+ *   invert = 1: lower triangle of A <- L^-1 (block Gauss-Jordan fused into the same sweep).
+ * The strictly upper triangle of A is never read or written (it keeps Sigma for the greedy
+ * nominators).  diag_out ([batch][n], or NULL) receives diag(L) (log-det).  info: [batch] int32.
+ * ws must hold vgposp_potrf_workspace_bytes(n).
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_potrf_workspace_bytes(int64_t n);
+int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t stride, int batch, int invert,
+                       double* diag_out, int* info, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * GP log marginal likelihood from the inverted factor.  Replaces
+ * tfd.GaussianProcess(...).log_prob(y) (gp_functions.py:166-172, main.py:105):
+ *     z = Minv y,   out[b] = -0.5 |z|^2 - sum_i log Ldiag[b][i] - n/2 log(2 pi)
+ * Minv: output of vgposp_potrf_lower(invert=1); Ldiag: its diag_out; y: [n] (shared over batch).
+ * alpha ([batch][n] or NULL) <- C^-1 y = Minv^T z.  ws: vgposp_lml_workspace_bytes(n, batch).
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_lml_workspace_bytes(int64_t n, int batch);
+int vgposp_lml(const double* Minv, int64_t n, int64_t lda, int64_t stride, int batch,
+               const double* Ldiag, const double* y, double* alpha, double* out, void* ws,
+               size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Gradient of the LML w.r.t. (amp[b], ls[b], noise) for the kernel family `kind`:
+ *     dLML/dtheta = 0.5 * sum_ij (alpha alpha^T - C^-1)_ij dC_ij/dtheta
+ * Cinv: the full C^-1 (lower triangle suffices; formed by vgposp_gemm(transa=1, tri) from Minv).
+ * grad: [batch][3] = (d/damp, d/dls, d/dnoise).  Replaces TF autodiff of
+ * tf_train_gp_adam's loss (gp_functions.py:179-182).
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_lml_grad_workspace_bytes(int64_t n, int batch);
+int vgposp_lml_grad(int kind, const double* X, int64_t n, int d, const double* amp,
+                    const double* ls, const double* Cinv, int64_t ldc, int64_t stride_c,
+                    const double* alpha, int batch, double* grad, void* ws, size_t ws_bytes,
+                    void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Greedy mutual-information placement (Krause, Singh & Guestrin Alg. 2 as implemented by
+ * placement_algorithm2.placement_algorithm_2, placement_algorithm2.py:151-219; lazy = 0 gives
+ * placement_algorithm_1, :128-145).  Same selections: delta_y = nom/denom with
+ *   nom   = sigma_yy - Sigma_yA Sigma_AA^-1 Sigma_Ay                    (nominator, :371-388)
+ *   denom = conditional variance of y given V \ (A u {y})               (denominator, :408-413)
+ * zeroed when |nom| < 1e-8 or |denom| < 1e-8 (:198); the lazy cache starts at +inf and every
+ * round re-scores the stale arg-max until the arg-max is fresh (:173-208); ties -> lowest index.
+ *
+ * Sigma: n x n row-major covariance (cov_vv) on device, lda >= n.  vgposp_greedy_init factors it
+ * IN PLACE (lower triangle <- L^-1, diagonal saved in ws; the strictly upper triangle must hold
+ * Sigma and is kept).  vgposp_greedy_step performs one selection round (round = 0, 1, ...).
+ * selected: int64 [kmax] device; sel_delta: f64 [kmax] device (delta of each pick) or NULL;
+ * info: int32 device (Cholesky status of init).  evals: int64 [kmax] device or NULL (number of
+ * delta evaluations the reference would have made in each round).
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_greedy_workspace_bytes(int64_t n, int kmax);
+int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kmax, int* info, void* ws,
+                       size_t ws_bytes, void* stream);
+int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, int round, int lazy,
+                       int64_t* selected, double* sel_delta, int64_t* evals, void* ws,
+                       size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VGPOSP_H_ */

@@ -1,0 +1,131 @@
+"""GPU parity: kernel assembly, MFMA GEMM, Cholesky (+ fused inverse), LML vs the CPU oracle."""
+import numpy as np
+import pytest
+
+from oracle import gp as ogp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    import torch
+    from vgposp_amd import linalg
+    torch.cuda.set_device(0)
+    return linalg
+
+
+@pytest.mark.parametrize("kind", ["eq", "matern12", "matern32", "matern52"])
+@pytest.mark.parametrize("d,n1,n2", [(1, 7, 300), (2, 130, 129), (3, 513, 257), (5, 33, 64)])
+def test_kernel_matrix(L, kind, d, n1, n2):
+    rng = np.random.default_rng(d * 1000 + n1)
+    X1 = rng.uniform(-2, 2, (n1, d))
+    X2 = rng.uniform(-2, 2, (n2, d))
+    amp, ls = [0.7, 1.3], [0.4, 1.9]
+    K = L.kernel_matrix(kind, X1, X2, amp, ls).cpu().numpy()
+    ref = ogp.kernel_matrix(kind, X1, X2, amp, ls)
+    np.testing.assert_allclose(K, ref, rtol=2e-14, atol=1e-300)
+
+
+@pytest.mark.parametrize("n", [1, 31, 200])
+def test_kernel_matrix_lower_and_shift(L, n):
+    import torch
+    rng = np.random.default_rng(n)
+    X = rng.uniform(-2, 2, (n, 3))
+    out = torch.full((1, n, n), 7.0, dtype=torch.float64, device="cuda")
+    L.kernel_matrix("eq", X, None, 1.1, 0.6, diag_shift=0.25, lower=True, out=out)
+    K = out[0].cpu().numpy()
+    ref = ogp.kernel_matrix("eq", X, X, 1.1, 0.6)[0] + 0.25 * np.eye(n)
+    il = np.tril_indices(n)
+    np.testing.assert_allclose(K[il], ref[il], rtol=2e-14)
+    iu = np.triu_indices(n, 1)
+    assert np.all(K[iu] == 7.0)  # upper triangle untouched
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("m,n,k", [(1, 1, 1), (17, 33, 5), (128, 128, 16), (130, 257, 300)])
+def test_gemm(L, ta, tb, m, n, k):
+    rng = np.random.default_rng(m + 7 * n + 13 * k + ta + 2 * tb)
+    A = rng.standard_normal((k, m) if ta else (m, k))
+    B = rng.standard_normal((n, k) if tb else (k, n))
+    C0 = rng.standard_normal((m, n))
+    opA = A.T if ta else A
+    opB = B.T if tb else B
+    C = L.as_device(C0.copy())
+    L.gemm(A, B, C, alpha=-1.5, beta=0.5, transa=bool(ta), transb=bool(tb))
+    np.testing.assert_allclose(C.cpu().numpy(), -1.5 * opA @ opB + 0.5 * C0, rtol=1e-12, atol=1e-12)
+
+
+def test_gemm_asymmetric_layout(L):
+    """A = I with an asymmetric B catches a transposed C/D fragment map."""
+    A = np.eye(16)
+    B = np.arange(16 * 16, dtype=np.float64).reshape(16, 16)
+    np.testing.assert_array_equal(L.gemm(A, B).cpu().numpy(), B)
+    np.testing.assert_array_equal(L.gemm(B, A).cpu().numpy(), B)
+
+
+@pytest.mark.parametrize("n", [40, 300])
+def test_gemm_lower_tri(L, n):
+    rng = np.random.default_rng(n)
+    M = np.tril(rng.standard_normal((n, n)))
+    Mstore = M + np.triu(rng.standard_normal((n, n)), 1) * 1e3  # garbage above the diagonal
+    Q = L.as_device(np.full((n, n), 5.0))
+    L.gemm(Mstore, Mstore, Q, transa=True, lower_c=True, tri_a=True, tri_b=True)
+    Qh = Q.cpu().numpy()
+    il = np.tril_indices(n)
+    np.testing.assert_allclose(Qh[il], (M.T @ M)[il], rtol=1e-12, atol=1e-12)
+    assert np.all(Qh[np.triu_indices(n, 1)] == 5.0)
+
+
+def _spd(n, rng):
+    X = rng.uniform(-2, 2, (n, 3))
+    return ogp.kernel_matrix("eq", X, X, 1.0, 0.7)[0] + 0.05 * np.eye(n)
+
+
+@pytest.mark.parametrize("n", [1, 5, 127, 128, 129, 300, 1000])
+@pytest.mark.parametrize("invert", [False, True])
+def test_cholesky(L, n, invert):
+    rng = np.random.default_rng(n)
+    S = _spd(n, rng)
+    U = np.triu(S, 1)
+    A = L.as_device(S.copy())
+    A, ld, _ = L.cholesky_(A, invert=invert)
+    Ah = A.cpu().numpy()
+    Lref = np.linalg.cholesky(S)
+    ref = np.linalg.inv(Lref) if invert else Lref
+    il = np.tril_indices(n)
+    np.testing.assert_allclose(Ah[il], ref[il], rtol=1e-9, atol=1e-10 * np.abs(ref).max())
+    np.testing.assert_array_equal(np.triu(Ah, 1), U)  # strictly upper untouched
+    np.testing.assert_allclose(ld[0].cpu().numpy(), np.diag(Lref), rtol=1e-12)
+
+
+def test_cholesky_batched_and_not_pd(L):
+    rng = np.random.default_rng(3)
+    S1, S2 = _spd(200, rng), _spd(200, rng)
+    S2[150, 150] = -1.0
+    A = L.as_device(np.stack([S1, S2]))
+    with pytest.raises(L.CholeskyError) as ei:
+        L.cholesky_(A)
+    assert ei.value.batch_index == 1 and ei.value.info >= 1
+    A = L.as_device(np.stack([S1, S1 * 2]))
+    L.cholesky_(A)
+    np.testing.assert_allclose(np.tril(A[1].cpu().numpy()), np.linalg.cholesky(2 * S1), rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["eq", "matern12", "matern52"])
+@pytest.mark.parametrize("n", [64, 300])
+def test_lml_and_grad(L, kind, n):
+    rng = np.random.default_rng(n)
+    X = rng.uniform(-2, 2, (n, 2))
+    y = np.sin(2 * np.pi * X).sum(1) + rng.normal(0, 0.03, n)
+    amp, ls, noise = [0.8, 1.2], [0.3, 0.9], 0.05
+    C = L.kernel_matrix(kind, X, None, amp, ls, diag_shift=noise + 1e-6, lower=True)
+    C, ld, _ = L.cholesky_(C, invert=True)
+    lml, alpha = L.lml_from_inverse(C, ld, y, want_alpha=True)
+    Q = L.inverse_from_factor_inverse(C)
+    g = L.lml_grad(kind, X, amp, ls, Q, alpha).cpu().numpy()
+    rl, ga, gl, gn = ogp.gp_log_prob_and_grads(kind, X, y, amp, ls, noise)
+    np.testing.assert_allclose(lml.cpu().numpy(), rl, rtol=1e-10)
+    np.testing.assert_allclose(g[:, 0], ga, rtol=1e-8)
+    np.testing.assert_allclose(g[:, 1], gl, rtol=1e-8)
+    np.testing.assert_allclose(g[:, 2], gn, rtol=1e-8)

@@ -1,0 +1,81 @@
+"""GPU parity of the greedy MI placement against the reference's golden vectors and the oracle."""
+import numpy as np
+import pytest
+
+from oracle import gp as ogp
+from oracle import placement as op
+from tests.golden_io import placement_cases, placement_cov
+
+pytestmark = pytest.mark.gpu
+CASES = placement_cases()
+
+
+@pytest.fixture(scope="module")
+def P():
+    import torch
+    from vgposp_amd import placement_algorithm2
+    torch.cuda.set_device(0)
+    return placement_algorithm2
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_golden_alg2(P, name):
+    e = CASES[name]
+    cov = placement_cov(name, e)
+    assert [int(a) for a in P.placement_algorithm_2(cov, e["k"])] == e["alg2"]
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if "alg1" in CASES[n]])
+def test_golden_alg1(P, name):
+    e = CASES[name]
+    assert [int(a) for a in P.placement_algorithm_1(placement_cov(name, e), e["k"])] == e["alg1"]
+
+
+@pytest.mark.parametrize("name", ["grid5", "grid654", "spd40", "grid8"])
+def test_golden_deltas_and_eval_counts(P, name):
+    """Selected deltas and the number of evaluations per round equal the reference's trace."""
+    e = CASES[name]
+    g = P.GreedyPlacement(placement_cov(name, e), e["k"], copy=True).run()
+    A, deltas, evals = g.result()
+    trace = e["trace"]
+    ref_sel_delta, ref_evals, last, cnt = [], [], {}, 0
+    for t in trace:
+        if t[0] == "select":
+            ref_sel_delta.append(last[t[1]])
+            ref_evals.append(cnt)
+            cnt = 0
+        else:
+            last[t[0]] = t[1]
+            cnt += 1
+    assert [int(a) for a in A] == e["alg2"]
+    np.testing.assert_allclose(deltas, ref_sel_delta, rtol=1e-9)
+    assert list(evals) == ref_evals
+
+
+@pytest.mark.parametrize("shape,kind,k", [((10, 10, 10), "eq", 12), ((20, 10, 8), "matern52", 10),
+                                          ((13, 11, 9), "matern12", 15)])
+def test_grid_vs_precision_oracle(P, shape, kind, k):
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    X = grid_points(shape, jitter=0.05, seed=3)
+    K = ogp.kernel_matrix(kind, X, X, 1.0, 2 * grid_spacing(shape))[0] + 0.010001 * np.eye(len(X))
+    got = [int(a) for a in P.placement_algorithm_2(K, k)]
+    assert got == op.placement_lazy_precision(K, k)
+    assert [int(a) for a in P.placement_algorithm_1(K, k)] == op.placement_lazy_precision(K, k, lazy=False)
+
+
+def test_device_assembled_sigma_matches(P):
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    shape = (9, 8, 7)
+    X = grid_points(shape, jitter=0.05, seed=5)
+    ls = 2 * grid_spacing(shape)
+    got = [int(a) for a in P.placement_from_points(X, 10, "eq", 1.0, ls, 1e-2)]
+    K = ogp.kernel_matrix("eq", X, X, 1.0, ls)[0] + (1e-2 + 1e-6) * np.eye(len(X))
+    assert got == op.placement_lazy_precision(K, 10)
+
+
+def test_k_equals_n_and_tiny(P):
+    cov = P.cov_vv_4x4()
+    assert [int(a) for a in P.placement_algorithm_2(cov, 1)] == [2]
+    assert [int(a) for a in P.placement_algorithm_2(np.array([[2.0]]), 1)] == [0]
+    with pytest.raises(ValueError):
+        P.placement_algorithm_2(cov, 5)

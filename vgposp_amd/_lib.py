@@ -1,0 +1,129 @@
+"""ctypes binding of libvgposp.so (the C-ABI declared in include/vgposp.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C vgposp_amd/csrc``).  There
+is no fallback: if the shared object is missing or cannot be loaded, every entry point raises
+``VgpospUnavailable`` — the product path never silently degrades to a CPU implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VGPOSP_LIB", os.path.join(_HERE, "libvgposp.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "vgposp.h")
+
+ABI_VERSION = 1
+E_HIP = -100
+E_WS = -101
+
+KERNEL_KINDS = {"eq": 0, "matern12": 1, "matern32": 2, "matern52": 3}
+FULL, LOWER = 0, 1
+
+
+class VgpospError(RuntimeError):
+    """A libvgposp entry point returned a non-zero status."""
+
+
+class VgpospUnavailable(VgpospError):
+    """libvgposp.so is missing or failed to load (build it with __graft_entry__.build())."""
+
+
+class CholeskyError(VgpospError):
+    """Mirror of TF's InvalidArgumentError 'Cholesky decomposition was not successful.'"""
+
+    def __init__(self, info, batch_index=0):
+        super().__init__(
+            "Cholesky decomposition was not successful. The input might not be valid. "
+            f"(leading minor of order {info} is not positive definite, batch {batch_index})")
+        self.info = int(info)
+        self.batch_index = int(batch_index)
+
+
+_c_void_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f64 = ctypes.c_double
+_size = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "vgposp_abi_version": (_i32, []),
+    "vgposp_last_error": (ctypes.c_char_p, []),
+    "vgposp_kernel_matrix": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p,
+                                    _c_void_p, _c_void_p, _i32, _i32, _c_void_p, _i64, _i64,
+                                    _c_void_p]),
+    "vgposp_gemm": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p, _i64,
+                           _f64, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p]),
+    "vgposp_potrf_workspace_bytes": (_size, [_i64]),
+    "vgposp_potrf_lower": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p,
+                                  _c_void_p, _size, _c_void_p]),
+    "vgposp_lml_workspace_bytes": (_size, [_i64, _i32]),
+    "vgposp_lml": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
+                          _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_lml_grad_workspace_bytes": (_size, [_i64, _i32]),
+    "vgposp_lml_grad": (_i32, [_i32, _c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p, _i64,
+                               _i64, _c_void_p, _i32, _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_workspace_bytes": (_size, [_i64, _i32]),
+    "vgposp_greedy_init": (_i32, [_c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p, _size,
+                                  _c_void_p]),
+    "vgposp_greedy_step": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
+                                  _c_void_p, _c_void_p, _size, _c_void_p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def header_symbols(path=HEADER_PATH):
+    """Function names declared in include/vgposp.h."""
+    with open(path) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(vgposp_[a-z0-9_]+)\s*\(", text)))
+
+
+def load():
+    """Load libvgposp.so once (raises VgpospUnavailable if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise VgpospUnavailable(
+                f"{LIB_PATH} not found: build the HIP library first (python -c "
+                "'import __graft_entry__ as g; g.build()')")
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover
+            raise VgpospUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.vgposp_abi_version()
+        if v != ABI_VERSION:
+            raise VgpospUnavailable(f"libvgposp ABI {v} != expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def last_error():
+    return load().vgposp_last_error().decode(errors="replace")
+
+
+def call(name, *args):
+    """Call an int-returning entry point; raise VgpospError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise VgpospError(f"{name} failed (rc={rc}): {last_error()}")
+    return rc
+
+
+def query(name, *args):
+    """Call a size-returning query (workspace sizes)."""
+    return int(getattr(load(), name)(*args))

@@ -1,0 +1,78 @@
+// Shared helpers for the vgposp HIP library (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/vgposp.h"
+
+namespace vgposp {
+
+// Thread-local last error message (vgposp_last_error()).
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define VG_CHECK_ARG(cond, idx)                                                       \
+  do {                                                                                \
+    if (!(cond)) {                                                                    \
+      ::vgposp::set_error("%s: bad argument %d (%s)", __func__, (idx), #cond);        \
+      return -(idx);                                                                  \
+    }                                                                                 \
+  } while (0)
+
+#define VG_HIP(expr)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      ::vgposp::set_error("%s: HIP error %s at %s:%d", __func__, hipGetErrorString(_e), \
+                          __FILE__, __LINE__);                                        \
+      return VGPOSP_E_HIP;                                                            \
+    }                                                                                 \
+  } while (0)
+
+#define VG_LAUNCH_CHECK() VG_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---- device helpers -------------------------------------------------------------------------
+
+// Wave64 reductions.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// (value, index) arg-max with the reference's tie rule: larger value wins; on equal value the
+// LOWER index wins (placement_algorithm2.py:62 uses strict '<' scanning upward).  Index -1 is
+// "no candidate" and loses to everything.  NaN values never win (comparisons are false).
+struct KeyMax {
+  double v;
+  long long i;
+};
+
+__device__ __forceinline__ bool key_gt(double v1, long long i1, double v2, long long i2) {
+  if (i1 < 0) return false;
+  if (i2 < 0) return true;
+  return (v1 > v2) || (v1 == v2 && i1 < i2);
+}
+
+__device__ __forceinline__ void wave_keymax(double& v, long long& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ov = __shfl_xor(v, o, 64);
+    long long oi = __shfl_xor(i, o, 64);
+    if (key_gt(ov, oi, v, i)) {
+      v = ov;
+      i = oi;
+    }
+  }
+}
+
+}  // namespace vgposp

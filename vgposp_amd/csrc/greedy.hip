@@ -1,0 +1,400 @@
+// Greedy mutual-information sensor placement, dense-exact, all on device.
+//
+// The reference (placement_algorithm2.py:151-219) evaluates, per candidate y,
+//   nom_y   = sigma_yy - Sigma_yA pinv(Sigma_AA) Sigma_Ay                 (:371-388)
+//   denom_y = sigma_yy - Sigma_yAbar pinv(Sigma_AbarAbar) Sigma_Abary     (:408-413)
+// with an SVD pinv of an (N-|A|-1)^2 matrix per evaluation.  Here both are maintained for ALL
+// candidates incrementally:
+//   * Sigma = L L^T is factored once and inverted in the same sweep (potrf.hip): M = L^-1 in the
+//     lower triangle, Sigma kept in the strictly upper triangle, diag(Sigma) saved.
+//   * nom: rank-1 Cholesky rows W (W[t] = L_AA^-1 Sigma_{A,:} row t): nom_y -= w_y^2.
+//   * denom = 1 / P_yy with P = (Sigma_SS)^-1, S = V \ A.  P_yy starts at Q_yy = |M e_y|^2 and is
+//     downdated per selection with q = Q e_a = M^T (M e_a) (one triangular mat-vec, the HBM-bound
+//     step) through rows V (V[t] = L_{Q_AA}^-1 Q_{A,:}): P_yy -= v_y^2.
+// The lazy cache policy is emulated exactly: fresh deltas are computed for every candidate, every
+// stale entry whose key exceeds the best fresh key is refreshed in bulk (the reference would refresh
+// all of them before it could stop), and the remaining re-score loop runs in one workgroup over
+// per-chunk maxima.  Keys order by value, ties by LOWER index (argmax_cache_linear, :53-67).
+#include <cfloat>
+
+#include "common.h"
+
+namespace vgposp {
+
+int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
+              double* linv, hipStream_t stream);
+size_t potrf_ws_bytes();
+
+constexpr int RC = 512;     // rows per chunk of the transposed mat-vec
+constexpr int CT = 256;     // columns per mat-vec workgroup
+constexpr int CH = 1024;    // candidates per chunk / per update workgroup
+constexpr int MAXCH = 2048; // chunks held in LDS by the select kernel -> n <= 2^21
+constexpr double DELTA_EPS = 1e-8;  // placement_algorithm2.py:198
+
+struct GreedyWS {
+  double *sdiag, *nom, *prec, *delta, *cache, *W, *V, *part, *xcol, *piv, *fval, *cval;
+  long long *fidx, *cidx, *cnt;
+  unsigned char *fresh, *selmask;
+  size_t bytes;
+};
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static GreedyWS greedy_layout(void* base, int64_t n, int kmax) {
+  GreedyWS w{};
+  const int64_t nrc = ceil_div(n, RC), nch = ceil_div(n, CH);
+  char* p = static_cast<char*>(base);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* r = p ? p + off : nullptr;
+    off += align_up(bytes);
+    return r;
+  };
+  w.sdiag = (double*)take(n * 8);
+  w.nom = (double*)take(n * 8);
+  w.prec = (double*)take(n * 8);
+  w.delta = (double*)take(n * 8);
+  w.cache = (double*)take(n * 8);
+  w.W = (double*)take((size_t)kmax * n * 8);
+  w.V = (double*)take((size_t)kmax * n * 8);
+  w.part = (double*)take((size_t)nrc * n * 8);
+  w.xcol = (double*)take(n * 8);
+  w.piv = (double*)take((2 + 2 * (size_t)kmax) * 8);
+  w.fval = (double*)take(nch * 8);
+  w.fidx = (long long*)take(nch * 8);
+  w.cval = (double*)take(nch * 8);
+  w.cidx = (long long*)take(nch * 8);
+  w.cnt = (long long*)take(8 * 8);
+  w.fresh = (unsigned char*)take(n);
+  w.selmask = (unsigned char*)take(n);
+  (void)take(potrf_ws_bytes());  // Linv scratch for the factorization (last)
+  w.bytes = off;
+  return w;
+}
+
+static double* greedy_linv(void* base, const GreedyWS& w) {
+  return reinterpret_cast<double*>(static_cast<char*>(base) + w.bytes - align_up(potrf_ws_bytes()));
+}
+
+// Block-wide (value, index) arg-max for blockDim == 1024.  Result valid in all threads.
+__device__ __forceinline__ void block_keymax(double& v, long long& i) {
+  __shared__ double sv[16];
+  __shared__ long long si[16];
+  wave_keymax(v, i);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) {
+    sv[w] = v;
+    si[w] = i;
+  }
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+  v = (l < nw) ? sv[l] : -DBL_MAX;
+  i = (l < nw) ? si[l] : -1;
+  wave_keymax(v, i);  // every wave reduces the same 16 entries
+}
+
+__global__ void greedy_init_kernel(const double* S, int64_t n, int64_t lda, GreedyWS w) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    w.sdiag[i] = S[i * lda + i];
+    w.cache[i] = __builtin_huge_val();  // INF = 1e1000 (placement_algorithm2.py:164)
+    w.selmask[i] = 0;
+  }
+  if (i < 8) w.cnt[i] = 0;
+}
+
+// x = M e_a restricted to rows >= a (the selected column of L^-1), a = selected[round-1].
+__global__ void greedy_extract_kernel(const double* M, int64_t n, int64_t lda,
+                                      const int64_t* selected, int round, double* xcol) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t a = selected[round - 1];
+  if (r < n) xcol[r] = (r >= a) ? M[r * lda + a] : 0.0;
+}
+
+// part[rc][c] = sum_{r in chunk rc, r >= max(c, a)} M[r][c] * f(r, c)
+//   SQ: f = M[r][c]          (column norms: Q_cc = |M e_c|^2)
+//   else f = xcol[r]          (q = M^T x)
+template <bool SQ>
+__global__ __launch_bounds__(CT) void greedy_trmv_kernel(const double* M, int64_t n, int64_t lda,
+                                                         const int64_t* selected, int round,
+                                                         const double* xcol, double* part) {
+  const int64_t c0 = (int64_t)blockIdx.x * CT;
+  const int64_t r0 = (int64_t)blockIdx.y * RC;
+  const int64_t r1 = min(r0 + RC, n);
+  if (c0 >= r1) return;  // tile strictly above the diagonal: never read by the reducer
+  const int64_t a = SQ ? 0 : selected[round - 1];
+  const int64_t c = c0 + threadIdx.x;
+  double acc0 = 0.0, acc1 = 0.0;
+  if (c < n) {
+    int64_t r = max(max(r0, a), c);
+    const double* p = M + r * lda + c;
+    for (; r + 1 < r1; r += 2, p += 2 * lda) {
+      const double m0 = p[0], m1 = p[lda];
+      if (SQ) {
+        acc0 += m0 * m0;
+        acc1 += m1 * m1;
+      } else {
+        acc0 += m0 * xcol[r];
+        acc1 += m1 * xcol[r + 1];
+      }
+    }
+    if (r < r1) {
+      const double m0 = p[0];
+      acc0 += SQ ? m0 * m0 : m0 * xcol[r];
+    }
+    part[blockIdx.y * n + c] = acc0 + acc1;
+  }
+}
+
+__device__ __forceinline__ double delta_of(double nom, double prec) {
+  const double den = 1.0 / prec;
+  if (fabs(den) < DELTA_EPS || fabs(nom) < DELTA_EPS) return 0.0;  // :198
+  return nom / den;
+}
+
+// Round 0: nom = diag(Sigma), prec = Q_ii.  Round t>0: rank-1 updates with a = selected[t-1].
+// Then delta for every unselected candidate and per-workgroup best fresh key.
+__global__ __launch_bounds__(CH) void greedy_update_kernel(const double* S, int64_t n, int64_t lda,
+                                                           const int64_t* selected, int round,
+                                                           GreedyWS w) {
+  const int64_t i = (int64_t)blockIdx.x * CH + threadIdx.x;
+  double bv = -DBL_MAX;
+  long long bi = -1;
+  if (i < n) {
+    const int64_t nrc = (n + RC - 1) / RC;
+    double q = 0.0;
+    if (round == 0) {
+      for (int64_t rc = i / RC; rc < nrc; ++rc) q += w.part[rc * n + i];
+      w.prec[i] = q;
+      w.nom[i] = w.sdiag[i];
+    } else {
+      const int64_t a = selected[round - 1];
+      const int t1 = round - 1;  // new row index in W / V
+      for (int64_t rc = max(i, a) / RC; rc < nrc; ++rc) q += w.part[rc * n + i];
+      double s = (i < a) ? S[i * lda + a] : (i > a ? S[a * lda + i] : w.sdiag[a]);
+      for (int t = 0; t < t1; ++t) {
+        s -= w.piv[2 + t] * w.W[(int64_t)t * n + i];
+        q -= w.piv[2 + t1 + t] * w.V[(int64_t)t * n + i];
+      }
+      const double noma = w.piv[0], preca = w.piv[1];
+      const double wy = noma > 0.0 ? s / sqrt(noma) : 0.0;
+      const double vy = preca > 0.0 ? q / sqrt(preca) : 0.0;
+      w.W[(int64_t)t1 * n + i] = wy;
+      w.V[(int64_t)t1 * n + i] = vy;
+      w.nom[i] -= wy * wy;
+      w.prec[i] -= vy * vy;
+    }
+    if (!w.selmask[i]) {
+      const double d = delta_of(w.nom[i], w.prec[i]);
+      w.delta[i] = d;
+      bv = d;
+      bi = i;
+    }
+  }
+  block_keymax(bv, bi);
+  if (threadIdx.x == 0) {
+    w.fval[blockIdx.x] = bv;
+    w.fidx[blockIdx.x] = bi;
+  }
+}
+
+// Reduce the nf per-workgroup keys in `val/idx` (all threads get the result).
+__device__ __forceinline__ void reduce_keys(const double* val, const long long* idx, int64_t nf,
+                                            double& v, long long& i) {
+  v = -DBL_MAX;
+  i = -1;
+  for (int64_t e = threadIdx.x; e < nf; e += blockDim.x) {
+    if (key_gt(val[e], idx[e], v, i)) {
+      v = val[e];
+      i = idx[e];
+    }
+  }
+  block_keymax(v, i);
+}
+
+// Bulk refresh: stale entries with key > best fresh key F* are re-scored (guaranteed by the
+// reference's loop before it can stop), then per-chunk maxima of the cache.
+__global__ __launch_bounds__(CH) void greedy_refresh_kernel(int64_t n, GreedyWS w) {
+  const int64_t nch = (n + CH - 1) / CH;
+  double fv;
+  long long fi;
+  reduce_keys(w.fval, w.fidx, nch, fv, fi);
+  const int64_t i = (int64_t)blockIdx.x * CH + threadIdx.x;
+  double bv = -DBL_MAX;
+  long long bi = -1;
+  int refreshed = 0;
+  if (i < n && !w.selmask[i]) {
+    double c = w.cache[i];
+    if (key_gt(c, i, fv, fi)) {
+      c = w.delta[i];
+      w.cache[i] = c;
+      w.fresh[i] = 1;
+      refreshed = 1;
+    } else {
+      w.fresh[i] = 0;
+    }
+    bv = c;
+    bi = i;
+  }
+  // count refreshes (one atomic per wave)
+  unsigned long long ball = __ballot(refreshed);
+  if ((threadIdx.x & 63) == 0 && ball) atomicAdd((unsigned long long*)&w.cnt[0], (unsigned long long)__popcll(ball));
+  block_keymax(bv, bi);
+  if (threadIdx.x == 0) {
+    w.cval[blockIdx.x] = bv;
+    w.cidx[blockIdx.x] = bi;
+  }
+}
+
+// One workgroup: the remaining re-score loop of placement_algorithm2.py:183-208, then selection.
+__global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round, int lazy,
+                                                           int64_t* selected, double* sel_delta,
+                                                           int64_t* evals, GreedyWS w) {
+  __shared__ double cv[MAXCH];
+  __shared__ long long ci[MAXCH];
+  __shared__ long long ychosen;
+  const int64_t nch = (n + CH - 1) / CH;
+  double v;
+  long long y = -1;
+  long long loop_evals = 0;
+  if (!lazy) {
+    reduce_keys(w.fval, w.fidx, nch, v, y);
+  } else {
+    for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) {
+      cv[c] = w.cval[c];
+      ci[c] = w.cidx[c];
+    }
+    __syncthreads();
+    for (int64_t it = 0; it <= n; ++it) {
+      reduce_keys(cv, ci, nch, v, y);
+      if (y < 0) break;
+      if (w.fresh[y]) break;  // arg-max is up to date -> select (:187-189)
+      // re-score y (:193-208) and recompute its chunk maximum
+      const double dy = w.delta[y];
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        w.cache[y] = dy;
+        w.fresh[y] = 1;
+      }
+      ++loop_evals;
+      __syncthreads();
+      const int64_t c = y / CH;
+      const int64_t j = c * CH + threadIdx.x;
+      double bv = -DBL_MAX;
+      long long bi = -1;
+      if (j < n && !w.selmask[j]) {
+        bv = (j == y) ? dy : w.cache[j];
+        bi = j;
+      }
+      block_keymax(bv, bi);
+      if (threadIdx.x == 0) {
+        cv[c] = bv;
+        ci[c] = bi;
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) ychosen = y;
+  __syncthreads();
+  y = ychosen;
+  if (y < 0) {
+    if (threadIdx.x == 0) {
+      selected[round] = -1;
+      if (sel_delta) sel_delta[round] = 0.0;
+    }
+    return;
+  }
+  // pivot data for the next update: nom_y, P_yy, W[0..round)[y], V[0..round)[y]
+  if (threadIdx.x == 0) {
+    selected[round] = y;
+    if (sel_delta) sel_delta[round] = w.delta[y];
+    if (evals) evals[round] = w.cnt[0] + loop_evals;
+    w.cnt[0] = 0;
+    w.selmask[y] = 1;
+    w.piv[0] = w.nom[y];
+    w.piv[1] = w.prec[y];
+  }
+  for (int t = threadIdx.x; t < round; t += blockDim.x) {
+    w.piv[2 + t] = w.W[(int64_t)t * n + y];
+    w.piv[2 + round + t] = w.V[(int64_t)t * n + y];
+  }
+}
+
+}  // namespace vgposp
+
+using namespace vgposp;
+
+extern "C" size_t vgposp_greedy_workspace_bytes(int64_t n, int kmax) {
+  if (n <= 0 || kmax <= 0) return 0;
+  return greedy_layout(nullptr, n, kmax).bytes;
+}
+
+extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kmax, int* info,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(Sigma != nullptr, 1);
+  VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
+  VG_CHECK_ARG(info != nullptr, 5);
+  VG_CHECK_ARG(ws != nullptr, 6);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  if (ws_bytes < w.bytes) {
+    set_error("vgposp_greedy_init: workspace %zu < %zu bytes", ws_bytes, w.bytes);
+    return VGPOSP_E_WS;
+  }
+  hipStream_t s = as_stream(stream);
+  VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
+  hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
+                     n, lda, w);
+  VG_LAUNCH_CHECK();
+  int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_linv(ws, w), s);
+  if (rc) return rc;
+  // Q_ii = |M e_i|^2 -> part (reduced in the round-0 update)
+  dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
+  hipLaunchKernelGGL(greedy_trmv_kernel<true>, g, dim3(CT), 0, s, Sigma, n, lda, nullptr, 0,
+                     nullptr, w.part);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
+                                  int lazy, int64_t* selected, double* sel_delta, int64_t* evals,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(Sigma != nullptr, 1);
+  VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
+  VG_CHECK_ARG(round >= 0 && round < kmax, 5);
+  VG_CHECK_ARG(selected != nullptr, 7);
+  VG_CHECK_ARG(ws != nullptr, 10);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  if (ws_bytes < w.bytes) {
+    set_error("vgposp_greedy_step: workspace %zu < %zu bytes", ws_bytes, w.bytes);
+    return VGPOSP_E_WS;
+  }
+  hipStream_t s = as_stream(stream);
+  const unsigned nch = (unsigned)ceil_div(n, CH);
+  if (round > 0) {
+    hipLaunchKernelGGL(greedy_extract_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                       Sigma, n, lda, selected, round, w.xcol);
+    VG_LAUNCH_CHECK();
+    dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
+    hipLaunchKernelGGL(greedy_trmv_kernel<false>, g, dim3(CT), 0, s, Sigma, n, lda, selected,
+                       round, w.xcol, w.part);
+    VG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(greedy_update_kernel, dim3(nch), dim3(CH), 0, s, Sigma, n, lda, selected,
+                     round, w);
+  VG_LAUNCH_CHECK();
+  if (lazy) {
+    hipLaunchKernelGGL(greedy_refresh_kernel, dim3(nch), dim3(CH), 0, s, n, w);
+    VG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(CH), 0, s, n, round, lazy, selected,
+                     sel_delta, evals, w);
+  VG_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,142 @@
+// PSD kernel assembly K(X1, X2) — HBM-write-bound (8 B written per entry, ~20-40 fp64 VALU ops for
+// the transcendental).  Replaces TFP's `kernel.matrix` for the kernels the reference builds
+// (gp_functions.py:160-163 MaternOneHalf, 3D_sin_wave.py:158-159 / main_tests.py:617
+// ExponentiatedQuadratic, main_architecture_2_sampledistribution.py:211 MaternFiveHalves), which
+// TF evaluates by materialising an [n, m, d] squared-difference tensor.
+//
+// Layout: each 256-thread workgroup writes a 32-row x 128-column tile; lane pairs of columns are
+// stored as one 16-byte write per row so a wave stores 1 KiB contiguous per row.  The X2 columns
+// of the tile are held in registers, X1 rows are wave-uniform (scalar-cached) loads.
+// Formula, as TFP evaluates it:  K = exp(2 log amp + log k(r / ls)).
+#include "common.h"
+
+namespace vgposp {
+
+constexpr int KM_ROWS = 32;
+constexpr int KM_COLS = 128;
+constexpr int KM_MAXD = 8;
+
+template <int KIND>
+__device__ __forceinline__ double kfun(double d2, double two_log_amp, double inv_ls, double inv_ls2) {
+  if (KIND == VGPOSP_KERNEL_EQ) {
+    return exp(two_log_amp - 0.5 * d2 * inv_ls2);
+  }
+  const double r = sqrt(d2) * inv_ls;
+  if (KIND == VGPOSP_KERNEL_MATERN12) return exp(two_log_amp - r);
+  if (KIND == VGPOSP_KERNEL_MATERN32) {
+    const double s = 1.7320508075688772 * r;
+    return exp(two_log_amp + log1p(s) - s);
+  }
+  const double s = 2.23606797749979 * r;  // MATERN52
+  return exp(two_log_amp + log1p(s + s * s * (1.0 / 3.0)) - s);
+}
+
+template <int KIND, int D>
+__global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, int64_t n1,
+                                                            const double* X2, int64_t n2, int d,
+                                                            const double* amp, const double* ls,
+                                                            const double* diag_shift, int uplo,
+                                                            double* K, int64_t ldk,
+                                                            int64_t stride_k, int vec) {
+  const int b = blockIdx.z;
+  const int64_t r0 = (int64_t)blockIdx.y * KM_ROWS;
+  const int64_t c0 = (int64_t)blockIdx.x * KM_COLS;
+  if (uplo == VGPOSP_LOWER && c0 > r0 + KM_ROWS - 1) return;
+  const int dd = D > 0 ? D : d;
+  const double a = amp[b], l = ls[b];
+  const double two_log_amp = 2.0 * log(a);
+  const double inv_ls = 1.0 / l;
+  const double inv_ls2 = 1.0 / (l * l);
+  const double shift = diag_shift ? diag_shift[b] : 0.0;
+  double* Kb = K + (int64_t)b * stride_k;
+
+  const int tx = threadIdx.x & 63;   // column pair
+  const int ty = threadIdx.x >> 6;   // row phase (0..3)
+  const int64_t ca = c0 + 2 * tx, cb = ca + 1;
+  double xa[KM_MAXD], xb[KM_MAXD];
+#pragma unroll
+  for (int k = 0; k < KM_MAXD; ++k) {
+    xa[k] = (k < dd && ca < n2) ? X2[ca * dd + k] : 0.0;
+    xb[k] = (k < dd && cb < n2) ? X2[cb * dd + k] : 0.0;
+  }
+#pragma unroll 2
+  for (int rr = 0; rr < KM_ROWS / 4; ++rr) {
+    const int64_t r = r0 + ty + 4 * rr;
+    if (r >= n1) break;
+    double da = 0.0, db = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM_MAXD; ++k) {
+      if (k < dd) {
+        const double xr = X1[r * dd + k];
+        const double ea = xr - xa[k], eb = xr - xb[k];
+        da += ea * ea;
+        db += eb * eb;
+      }
+    }
+    double va = kfun<KIND>(da, two_log_amp, inv_ls, inv_ls2);
+    double vb = kfun<KIND>(db, two_log_amp, inv_ls, inv_ls2);
+    if (diag_shift) {
+      if (ca == r) va += shift;
+      if (cb == r) vb += shift;
+    }
+    double* row = Kb + r * ldk;
+    const bool oka = ca < n2 && (uplo != VGPOSP_LOWER || ca <= r);
+    const bool okb = cb < n2 && (uplo != VGPOSP_LOWER || cb <= r);
+    if (vec && oka && okb) {
+      *reinterpret_cast<double2*>(row + ca) = make_double2(va, vb);
+    } else {
+      if (oka) row[ca] = va;
+      if (okb) row[cb] = vb;
+    }
+  }
+}
+
+template <int KIND>
+static void launch_kind(dim3 g, hipStream_t s, const double* X1, int64_t n1, const double* X2,
+                        int64_t n2, int d, const double* amp, const double* ls,
+                        const double* shift, int uplo, double* K, int64_t ldk, int64_t stride,
+                        int vec) {
+  switch (d) {
+    case 1: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 1>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
+    case 2: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 2>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
+    case 3: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 3>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
+    default: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 0>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
+  }
+}
+
+}  // namespace vgposp
+
+using namespace vgposp;
+
+extern "C" int vgposp_kernel_matrix(int kind, const double* X1, int64_t n1, const double* X2,
+                                    int64_t n2, int d, const double* amp, const double* ls,
+                                    const double* diag_shift, int batch, int uplo, double* K,
+                                    int64_t ldk, int64_t stride_k, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(kind >= VGPOSP_KERNEL_EQ && kind <= VGPOSP_KERNEL_MATERN52, 1);
+  VG_CHECK_ARG(X1 != nullptr || n1 == 0, 2);
+  VG_CHECK_ARG(n1 >= 0, 3);
+  VG_CHECK_ARG(X2 != nullptr || n2 == 0, 4);
+  VG_CHECK_ARG(n2 >= 0, 5);
+  VG_CHECK_ARG(d >= 1 && d <= KM_MAXD, 6);
+  VG_CHECK_ARG(amp != nullptr, 7);
+  VG_CHECK_ARG(ls != nullptr, 8);
+  VG_CHECK_ARG(batch >= 1 && batch <= 65535, 10);
+  VG_CHECK_ARG(uplo == VGPOSP_FULL || uplo == VGPOSP_LOWER, 11);
+  VG_CHECK_ARG(K != nullptr || n1 == 0 || n2 == 0, 12);
+  VG_CHECK_ARG(ldk >= n2, 13);
+  VG_CHECK_ARG(batch == 1 || stride_k >= ldk * n1, 14);
+  if (n1 == 0 || n2 == 0) return 0;
+  dim3 g((unsigned)ceil_div(n2, KM_COLS), (unsigned)ceil_div(n1, KM_ROWS), (unsigned)batch);
+  const int vec = (reinterpret_cast<uintptr_t>(K) % 16 == 0) && (ldk % 2 == 0) &&
+                  (batch == 1 || stride_k % 2 == 0);
+  hipStream_t s = as_stream(stream);
+  switch (kind) {
+    case VGPOSP_KERNEL_EQ: launch_kind<VGPOSP_KERNEL_EQ>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
+    case VGPOSP_KERNEL_MATERN12: launch_kind<VGPOSP_KERNEL_MATERN12>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
+    case VGPOSP_KERNEL_MATERN32: launch_kind<VGPOSP_KERNEL_MATERN32>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
+    default: launch_kind<VGPOSP_KERNEL_MATERN52>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
+  }
+  VG_LAUNCH_CHECK();
+  return 0;
+}
