@@ -1,0 +1,252 @@
+"""Benchmark of the hot path: greedy MI sensor placement on an N = 65,536-point 3-D grid
+(64 x 32 x 32, EQ kernel) — BASELINE.json's metric "greedy sensor placements/sec + fp64 Cholesky
+GF/s on N=65k 3D grid".
+
+One step = the whole job for one spatial split, with the grid points already resident in HBM:
+  assemble Sigma = K(X, X) + (noise + jitter) I  (kernel_matrix, HBM-write-bound)
+  -> fused Cholesky + inverse of Sigma             (potrf sweep, fp64 MFMA-bound, 2N^3/3 flops)
+  -> k = 50 lazy-greedy selections                 (per round one HBM-bound triangular mat-vec)
+value = placements per second of the whole job (all ranks).  With --gpus N every rank owns one
+64x32x32 split of a (64 N) x 32 x 32 domain (the reference splits its domain the same way,
+main_architecture_2_sampledistribution.py:987-989), so per-GPU work is fixed: weak scaling, no
+collective in the data path (only the timing barrier / max-reduction).
+
+Also reported: fp64 Cholesky GF/s (plain potrf of the same Sigma, N^3/3 flops), the roofline of
+the dominant kernel measured live with the library's HIP-event profiling, and a CPU baseline
+(the oracle's pinv-faithful restatement of placement_algorithm2.py timed on the host cores on a
+bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (spec), MI355X_MICROARCH.md
+METRIC = "greedy sensor placements/sec + fp64 Cholesky GF/s on N=65k 3D grid"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--shape", type=int, nargs=3, default=[64, 32, 32])
+    p.add_argument("--k", type=int, default=50)
+    p.add_argument("--kernel", default="eq")
+    p.add_argument("--noise", type=float, default=1e-2)
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    p.add_argument("--cpu-shape", type=int, nargs=3, default=[8, 8, 8])
+    p.add_argument("--cpu-k", type=int, default=2)
+    p.add_argument("--no-potrf", action="store_true", help="skip the separate potrf GF/s run")
+    return p.parse_args()
+
+
+def cpu_threads():
+    try:
+        from threadpoolctl import threadpool_info
+        n = [i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"]
+        if n:
+            return int(max(n))
+    except Exception:
+        pass
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, N):
+    """Oracle restatement of placement_algorithm2.placement_algorithm_2 (pinv per candidate, the
+    reference's algorithm) timed on the host on a bounded sample, plus OpenBLAS Cholesky GF/s."""
+    from oracle import gp as ogp
+    from oracle import placement as op
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+
+    shape = tuple(args.cpu_shape)
+    X = grid_points(shape, jitter=0.05, seed=0)
+    h = grid_spacing(shape)
+    S = ogp.kernel_matrix(args.kernel, X, X, 1.0, 2 * h)[0] + (args.noise + 1e-6) * np.eye(len(X))
+    trace = []
+    t0 = time.perf_counter()
+    op.placement_algorithm_2(S, args.cpu_k, trace=trace)
+    t = time.perf_counter() - t0
+    nevals = sum(1 for e in trace if e[0] != "select")
+    n_s = len(X)
+    t_eval = t / max(nevals, 1)
+    # round 1 alone needs N evaluations of an O(N^3) pinv: a lower bound on the time at N
+    t_lb = t_eval * (N / n_s) ** 3 * N
+    # OpenBLAS Cholesky of the same kernel family at a bounded size
+    nc = 6144
+    Xc = grid_points((24, 16, 16), jitter=0.0)
+    Sc = ogp.kernel_matrix(args.kernel, Xc, Xc, 1.0, 2 * grid_spacing((24, 16, 16)))[0]
+    Sc[np.diag_indices(nc)] += args.noise + 1e-6
+    t0 = time.perf_counter()
+    np.linalg.cholesky(Sc)
+    tc = time.perf_counter() - t0
+    return {
+        "value": args.cpu_k / t,
+        "unit": "placements/s",
+        "cores": cpu_threads(),
+        "kind": "port",
+        "sample": (f"oracle pinv restatement of placement_algorithm_2 on a jittered "
+                   f"{shape[0]}x{shape[1]}x{shape[2]} grid (N={n_s}), k={args.cpu_k}: {nevals} "
+                   f"delta evaluations in {t:.1f} s; numpy/OpenBLAS cholesky at N={nc}"),
+        "extrapolated_value_at_N": args.k / t_lb,
+        "cholesky_gflops": nc ** 3 / 3 / tc / 1e9,
+        "cpu_model": cpu_model(),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from vgposp_amd import _lib, linalg
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    from vgposp_amd.placement_algorithm2 import GreedyPlacement
+
+    shape = tuple(args.shape)
+    h = grid_spacing(shape)
+    X = grid_points(shape)
+    X[:, 0] += rank * shape[0] * h  # this rank's spatial split
+    N = X.shape[0]
+    k = args.k
+    ls = 2.0 * h
+    Xd = linalg.as_device(X)
+    amp_d = linalg.as_device([1.0])
+    ls_d = linalg.as_device([ls])
+    shift_d = linalg.as_device([args.noise + 1e-6])
+    Sigma = torch.empty((N, N), dtype=torch.float64, device="cuda")
+    g = GreedyPlacement(Sigma, k)  # Sigma is factored in place every step
+
+    def step():
+        linalg.kernel_matrix(args.kernel, Xd, None, amp_d, ls_d, diag_shift=shift_d, out=Sigma[None])
+        g.init()
+        for _ in range(k):
+            g.step(lazy=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    g.check()
+    ref_sel = g.selected.clone()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    _lib.prof_enable(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = {name: _lib.prof_query(name) for name in
+            ["kernel_matrix", "gemm_f64", "potrf_diag", "greedy_colsq", "greedy_trmv", "greedy_update"]}
+    _lib.prof_enable(False)
+    g.check()
+    deterministic = bool(torch.equal(ref_sel, g.selected))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # separate plain potrf (N^3/3) for the Cholesky GF/s figure
+    chol_gflops = None
+    if not args.no_potrf:
+        linalg.kernel_matrix(args.kernel, Xd, None, amp_d, ls_d, diag_shift=shift_d, lower=True,
+                             out=Sigma[None])
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        linalg.cholesky_(Sigma, invert=False, check=False)
+        ev1.record()
+        torch.cuda.synchronize()
+        chol_gflops = N ** 3 / 3 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * k * args.steps / elapsed
+    # dominant kernel by time over the timed region
+    dom = max(prof, key=lambda n: prof[n][0])
+    ms, launches, flops, nbytes = prof[dom]
+    if flops > 0 and dom == "gemm_f64":
+        achieved = flops / (ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": None}
+    else:
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
+    roof.update({"kernel": dom, "launches": launches, "avg_launch_ms": ms / max(launches, 1),
+                 "share_of_step": ms / (elapsed * 1e3)})
+    breakdown = {n: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[1] / args.steps,
+                     "achieved": (v[2] / (v[0] * 1e-3) / 1e12 if v[2] and n == "gemm_f64" else
+                                  v[3] / max(v[0], 1e-9) / 1e6),
+                     "unit": "TFLOP/s" if n == "gemm_f64" else "GB/s"}
+                 for n, v in prof.items() if v[1]}
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "placements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"{shape[0]}x{shape[1]}x{shape[2]} grid per split (N={N}), "
+                               f"{args.kernel.upper()} kernel amp=1 ls=2h noise={args.noise}+1e-6, "
+                               f"k={k} lazy-greedy MI placements, dense-exact",
+                   "N": N, "k": k, "splits": world, "parallelism": f"split{world}"},
+        "cholesky_gflops": chol_gflops,
+        "roofline": roof,
+        "breakdown": breakdown,
+        "deterministic_selection": deterministic,
+        "selected_head": [int(a) for a in g.selected[:8].cpu()],
+    }
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args, N)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -142,6 +142,18 @@ int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, in
                        int64_t* selected, double* sel_delta, int64_t* evals, void* ws,
                        size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Optional per-launch timing (no reference counterpart; the reference times with wall clocks,
+ * placement_algorithm2.py:416-430).  When enabled, every launch of the library's named kernels
+ * ("gemm_f64", "potrf_diag", "kernel_matrix", "greedy_trmv", "greedy_update", "greedy_select",
+ * ...) is bracketed by a hipEvent pair on its stream together with its algorithmic flops and
+ * bytes.  vgposp_prof_query synchronises on the recorded events and sums them per kernel name.
+ * Enabling (or re-enabling) clears the records.  Host-side state, guarded by a mutex.
+ * --------------------------------------------------------------------------------------------- */
+int vgposp_prof_enable(int on);
+int vgposp_prof_query(const char* name, double* total_ms, int64_t* launches, double* flops,
+                      double* bytes);
+
 #ifdef __cplusplus
 }
 #endif

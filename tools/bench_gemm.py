@@ -1,0 +1,42 @@
+"""Micro-benchmark of the fp64 MFMA GEMM (vgposp_gemm) on the shapes the Cholesky sweep uses."""
+import argparse
+import json
+import sys
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from vgposp_amd import linalg
+
+
+def run(m, n, k, ta, tb, lower, beta, reps=5):
+    A = torch.randn((k, m) if ta else (m, k), dtype=torch.float64, device="cuda")
+    B = torch.randn((n, k) if tb else (k, n), dtype=torch.float64, device="cuda")
+    C = torch.randn((m, n), dtype=torch.float64, device="cuda")
+    linalg.gemm(A, B, C, alpha=-1.0, beta=beta, transa=ta, transb=tb, lower_c=lower)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        linalg.gemm(A, B, C, alpha=-1.0, beta=beta, transa=ta, transb=tb, lower_c=lower)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / reps * 1e-3
+    outs = m * (m + 1) / 2 if lower else m * n
+    return {"m": m, "n": n, "k": k, "ta": ta, "tb": tb, "lower": lower, "ms": t * 1e3,
+            "tflops": 2 * k * outs / t / 1e12}
+
+
+if __name__ == "__main__":
+    shapes = [
+        (8192, 8192, 8192, 0, 1, False, 0.0),
+        (16384, 16384, 128, 0, 1, True, 1.0),    # trailing SYRK, K = 128
+        (16384, 16384, 256, 0, 1, True, 1.0),    # trailing SYRK, K = 256
+        (32768, 32768, 128, 0, 1, True, 1.0),
+        (16384, 16384, 128, 0, 0, False, 1.0),   # GJ update (NN)
+        (65536, 128, 128, 0, 1, False, 0.0),     # panel
+        (8192, 8192, 8192, 1, 0, True, 0.0),     # M^T M
+    ]
+    for s in shapes:
+        print(json.dumps(run(*s)), flush=True)

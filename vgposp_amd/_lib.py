@@ -69,6 +69,9 @@ SIGNATURES = {
     "vgposp_greedy_workspace_bytes": (_size, [_i64, _i32]),
     "vgposp_greedy_init": (_i32, [_c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p, _size,
                                   _c_void_p]),
+    "vgposp_prof_enable": (_i32, [_i32]),
+    "vgposp_prof_query": (_i32, [ctypes.c_char_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64),
+                                 ctypes.POINTER(_f64), ctypes.POINTER(_f64)]),
     "vgposp_greedy_step": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                   _c_void_p, _c_void_p, _size, _c_void_p]),
 }
@@ -127,3 +130,15 @@ def call(name, *args):
 def query(name, *args):
     """Call a size-returning query (workspace sizes)."""
     return int(getattr(load(), name)(*args))
+
+
+def prof_enable(on=True):
+    call("vgposp_prof_enable", int(on))
+
+
+def prof_query(name):
+    """(total_ms, launches, algorithmic_flops, algorithmic_bytes) of a kernel since prof_enable."""
+    ms, n, fl, by = _f64(), _i64(), _f64(), _f64()
+    call("vgposp_prof_query", name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
+         ctypes.byref(by))
+    return ms.value, n.value, fl.value, by.value

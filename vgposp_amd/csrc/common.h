@@ -76,3 +76,21 @@ __device__ __forceinline__ void wave_keymax(double& v, long long& i) {
 }
 
 }  // namespace vgposp
+
+namespace vgposp {
+// Optional per-launch timing (vgposp_prof_enable): the library records a hipEvent pair around
+// every launch of a named kernel together with its algorithmic flops / bytes.  Off by default.
+bool prof_on();
+int prof_begin(const char* name, hipStream_t s, double flops, double bytes);
+void prof_end(int slot, hipStream_t s);
+
+struct ProfScope {
+  int slot;
+  hipStream_t s;
+  ProfScope(const char* name, hipStream_t st, double flops, double bytes)
+      : slot(prof_on() ? prof_begin(name, st, flops, bytes) : -1), s(st) {}
+  ~ProfScope() {
+    if (slot >= 0) prof_end(slot, s);
+  }
+};
+}  // namespace vgposp

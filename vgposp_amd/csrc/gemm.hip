@@ -217,6 +217,9 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
   GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b};
   dim3 grid((unsigned)ceil_div(n, GBN), (unsigned)ceil_div(m, GBM));
   const int va = aligned16(A, lda), vb = aligned16(B, ldb);
+  const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
+  ProfScope ps("gemm_f64", stream, 2.0 * (double)k * outs,
+               8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
   if (!transa && !transb) hipLaunchKernelGGL((gemm_f64_kernel<false, false>), grid, dim3(256), 0, stream, p, va, vb);
   else if (!transa && transb) hipLaunchKernelGGL((gemm_f64_kernel<false, true>), grid, dim3(256), 0, stream, p, va, vb);
   else if (transa && !transb) hipLaunchKernelGGL((gemm_f64_kernel<true, false>), grid, dim3(256), 0, stream, p, va, vb);

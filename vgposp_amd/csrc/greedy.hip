@@ -353,6 +353,7 @@ extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kma
   if (rc) return rc;
   // Q_ii = |M e_i|^2 -> part (reduced in the round-0 update)
   dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
+  ProfScope ps("greedy_colsq", s, (double)n * (n + 1), 8.0 * (0.5 * (double)n * (n + 1) + (double)ceil_div(n, RC) * n));
   hipLaunchKernelGGL(greedy_trmv_kernel<true>, g, dim3(CT), 0, s, Sigma, n, lda, nullptr, 0,
                      nullptr, w.part);
   VG_LAUNCH_CHECK();
@@ -382,17 +383,25 @@ extern "C" int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, i
                        Sigma, n, lda, selected, round, w.xcol);
     VG_LAUNCH_CHECK();
     dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
+    // algorithmic: the lower triangle of L^-1 in rows >= a (a is device-side: count the mean,
+    // n(n+1)/2 * (1 - E[a^2]/n^2) is not known on the host, so report the full triangle)
+    ProfScope ps("greedy_trmv", s, (double)n * (n + 1), 8.0 * (0.5 * (double)n * (n + 1) + 2.0 * n));
     hipLaunchKernelGGL(greedy_trmv_kernel<false>, g, dim3(CT), 0, s, Sigma, n, lda, selected,
                        round, w.xcol, w.part);
     VG_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(greedy_update_kernel, dim3(nch), dim3(CH), 0, s, Sigma, n, lda, selected,
-                     round, w);
-  VG_LAUNCH_CHECK();
+  {
+    ProfScope psu("greedy_update", s, 0.0, 8.0 * (double)n * (6 + 2.0 * round));
+    hipLaunchKernelGGL(greedy_update_kernel, dim3(nch), dim3(CH), 0, s, Sigma, n, lda, selected,
+                       round, w);
+    VG_LAUNCH_CHECK();
+  }
   if (lazy) {
+    ProfScope psr("greedy_refresh", s, 0.0, 8.0 * 3.0 * n);
     hipLaunchKernelGGL(greedy_refresh_kernel, dim3(nch), dim3(CH), 0, s, n, w);
     VG_LAUNCH_CHECK();
   }
+  ProfScope pss("greedy_select", s, 0.0, 0.0);
   hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(CH), 0, s, n, round, lazy, selected,
                      sel_delta, evals, w);
   VG_LAUNCH_CHECK();

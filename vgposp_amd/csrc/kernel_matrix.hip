@@ -131,6 +131,8 @@ extern "C" int vgposp_kernel_matrix(int kind, const double* X1, int64_t n1, cons
   const int vec = (reinterpret_cast<uintptr_t>(K) % 16 == 0) && (ldk % 2 == 0) &&
                   (batch == 1 || stride_k % 2 == 0);
   hipStream_t s = as_stream(stream);
+  const double outs = (uplo == VGPOSP_LOWER) ? 0.5 * (double)n1 * (double)(n1 + 1) : (double)n1 * n2;
+  ProfScope ps("kernel_matrix", s, 0.0, 8.0 * (batch * outs + (double)d * (n1 + n2)));
   switch (kind) {
     case VGPOSP_KERNEL_EQ: launch_kind<VGPOSP_KERNEL_EQ>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
     case VGPOSP_KERNEL_MATERN12: launch_kind<VGPOSP_KERNEL_MATERN12>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;

@@ -121,9 +121,12 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
     const int jb = (int)(n - j0 < NB ? n - j0 : NB);
     const int64_t j1 = j0 + jb, m = n - j1;
     double* Ajj = A + j0 * lda + j0;
-    hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(DIAG_THREADS), shmem, stream, Ajj, lda,
-                       jb, j0, invert, linv, diag_out ? diag_out + j0 : nullptr, info);
-    VG_LAUNCH_CHECK();
+    {
+      ProfScope ps("potrf_diag", stream, 2.0 * jb * (double)jb * jb / 3.0, 8.0 * jb * (double)jb * 2);
+      hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(DIAG_THREADS), shmem, stream, Ajj, lda,
+                         jb, j0, invert, linv, diag_out ? diag_out + j0 : nullptr, info);
+      VG_LAUNCH_CHECK();
+    }
     double* A21 = A + j1 * lda + j0;
     int rc;
     if (m > 0) {
