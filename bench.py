@@ -134,8 +134,10 @@ def main():
 
     shape = tuple(args.shape)
     h = grid_spacing(shape)
-    X = grid_points(shape)
-    X[:, 0] += rank * shape[0] * h  # this rank's spatial split
+    # jittered grid (seed = rank) so the selections are decided by the data, not by the exact
+    # octant ties of a regular grid; this rank's split is shifted along axis 0
+    X = grid_points(shape, jitter=0.05, seed=rank)
+    X[:, 0] += rank * shape[0] * h
     N = X.shape[0]
     k = args.k
     ls = 2.0 * h

@@ -21,11 +21,14 @@ def test_abi_version():
 
 
 def test_workspace_queries():
-    assert _lib.query("vgposp_potrf_workspace_bytes", 1000) >= 128 * 128 * 8
+    # leaf inverses (ceil(n/128) x 128^2) + the trtri scratch of the top split (n1 x n2)
+    assert _lib.query("vgposp_potrf_workspace_bytes", 1000) >= (8 * 128 * 128 + 512 * 488) * 8
+    assert _lib.query("vgposp_potrf_workspace_bytes", 0) == 0
     n, k = 65536, 50
     ws = _lib.query("vgposp_greedy_workspace_bytes", n, k)
-    assert ws >= 2 * k * n * 8  # W and V rows
-    assert ws < 16 * n * 8 + 2 * k * n * 8 + (n // 512 + 1) * n * 8 + 2 ** 22
+    fact = _lib.query("vgposp_potrf_workspace_bytes", n)
+    assert ws >= 2 * k * n * 8 + fact  # W and V rows + factorization scratch
+    assert ws < 16 * n * 8 + 2 * k * n * 8 + (n // 512 + 1) * n * 8 + fact + 2 ** 22
     assert _lib.query("vgposp_greedy_workspace_bytes", 0, 5) == 0
     assert _lib.query("vgposp_lml_workspace_bytes", 100, 2) == 1600
 

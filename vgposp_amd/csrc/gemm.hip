@@ -112,7 +112,7 @@ __device__ __forceinline__ double frag(const double* lds, int row, int k) {
 
 // TA: A stored k x m (A^T used).  TB: B stored n x k (B^T used).
 template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p, int vec_a, int vec_b) {
+__global__ __launch_bounds__(256) void gemm_ref_kernel(GemmParams p, int vec_a, int vec_b) {
   constexpr bool A_KC = !TA;  // A[m][k] is k-contiguous
   constexpr bool B_KC = TB;   // B[n][k] is k-contiguous
   __shared__ double smem[2 * 2 * TILE_ELEMS];  // [buf][A|B][tile]
@@ -206,6 +206,195 @@ __global__ __launch_bounds__(256) void gemm_f64_kernel(GemmParams p, int vec_a, 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fast path: operands streamed HBM -> LDS with global_load_lds_dwordx4 (no VGPR staging) through
+// a STAGES-deep ring, counted vmcnt waits and raw barriers, so STAGES-1 K-tiles are in flight
+// while one is multiplied.  The LDS images are lane-linear (as glds requires) and the XOR swizzle
+// is applied on the per-lane SOURCE address and on the fragment read (conflict-free reads):
+//   KC image [128 rows][16 k]:  slot (r, pair p) holds pair p ^ ((r & 15) >> 1)
+//   MC image [16 k][128 cols]:  slot (k, pair p) holds pair p ^ ((k & 1) << 3)
+// Out-of-range rows / columns / k are CLAMPED to valid addresses (every load is in bounds); the
+// duplicated data is discarded at the store (rows, columns) or masked at the fragment read (k,
+// triangular operands).  Requires even m, n, k, ld and 16-byte aligned bases (else gemm_ref).
+// Workgroups are remapped XCD-aware (contiguous tile ranges per XCD) and, for a lower-triangular
+// C, only tiles on or below the diagonal are launched.
+constexpr int STAGES = 4;
+constexpr int OPND_ELEMS = GBM * GBK;        // 2048 doubles = 16 KiB per operand per stage
+constexpr int STAGE_ELEMS = 2 * OPND_ELEMS;  // A | B
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <bool KC>
+__device__ __forceinline__ void glds_operand(const double* base, int64_t ld, int64_t r0, int64_t k0,
+                                             int64_t R, int64_t K, double* dst, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = wave * 4 + j;  // wave-instruction index 0..15, 1 KiB each
+    const double* src;
+    if (KC) {
+      const int row = 8 * i + (lane >> 3);
+      const int kp = (lane & 7) ^ ((row & 15) >> 1);
+      const int64_t gr = min(r0 + row, R - 1);
+      const int64_t gk = min(k0 + 2 * kp, K - 2);
+      src = base + gr * ld + gk;
+    } else {
+      const int p = lane ^ ((i & 1) << 3);
+      const int64_t gk = min(k0 + i, K - 1);
+      const int64_t gc = min(r0 + 2 * p, R - 2);
+      src = base + gk * ld + gc;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(dst + i * 128), 16, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ int frag_off(int row, int k) {
+  if (KC) return row * 16 + 2 * ((k >> 1) ^ ((row & 15) >> 1)) + (k & 1);
+  return k * 128 + 2 * ((row >> 1) ^ ((k & 1) << 3)) + (row & 1);
+}
+
+__device__ __forceinline__ int tri_root(int64_t id) {
+  int64_t t = (int64_t)((sqrt(8.0 * (double)id + 1.0) - 1.0) * 0.5);
+  while ((t + 1) * (t + 2) / 2 <= id) ++t;
+  while (t * (t + 1) / 2 > id) --t;
+  return (int)t;
+}
+
+template <bool TA, bool TB, bool TRIA, bool TRIB>
+__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr bool A_KC = !TA;
+  constexpr bool B_KC = TB;
+  __shared__ double smem[STAGES * STAGE_ELEMS];
+
+  // XCD-aware bijective remap of the linear workgroup id.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  int ti, tj;
+  if (p.uplo_c == VGPOSP_LOWER) {
+    ti = tri_root(wg);
+    tj = wg - ti * (ti + 1) / 2;
+  } else {
+    constexpr int GROUP = 8;  // row tiles per group: neighbours share A rows and B columns
+    const int per_group = GROUP * tiles_n;
+    const int g = wg / per_group, first = g * GROUP;
+    const int gsize = min(GROUP, tiles_m - first);
+    const int local = wg - g * per_group;
+    ti = first + local % gsize;
+    tj = local / gsize;
+  }
+  const int64_t m0 = (int64_t)ti * GBM, n0 = (int64_t)tj * GBN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+
+  // K range that can contribute when an operand is stored lower triangular.
+  int64_t kbeg = 0, kend = p.k;
+  if (TRIA) {
+    if (TA) kbeg = max(kbeg, m0);        // stored A[k][i], zero for i > k
+    else kend = min(kend, m0 + GBM);     // stored A[i][k], zero for k > i
+  }
+  if (TRIB) {
+    if (TB) kend = min(kend, n0 + GBN);  // stored B[j][k], zero for k > j
+    else kbeg = max(kbeg, n0);           // stored B[k][j], zero for j > k
+  }
+  kbeg = (kbeg / GBK) * GBK;
+  if (kend < kbeg) kend = kbeg;
+  const int T = (int)((kend - kbeg + GBK - 1) / GBK);
+  const bool partial_last = ((kend - kbeg) % GBK) != 0;
+
+  dbl4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  auto issue = [&](int t) {
+    double* st = smem + (t % STAGES) * STAGE_ELEMS;
+    const int64_t k0 = kbeg + (int64_t)t * GBK;
+    glds_operand<A_KC>(p.A, p.lda, m0, k0, p.m, p.k, st, wave, lane);
+    glds_operand<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + OPND_ELEMS, wave, lane);
+  };
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < T) issue(s);
+
+  for (int t = 0; t < T; ++t) {
+    const int after = min(T - 1 - t, STAGES - 2);  // tiles that may stay in flight
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + STAGES - 1 < T) issue(t + STAGES - 1);
+
+    const double* As = smem + (t % STAGES) * STAGE_ELEMS;
+    const double* Bs = As + OPND_ELEMS;
+    const int64_t k0 = kbeg + (int64_t)t * GBK;
+    // masks only where needed: the last partial K-tile, and K-tiles that straddle the diagonal
+    // of a triangular operand (k0 within 128 of the tile's first row / column)
+    const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + GBM && k0 + GBK > m0) ||
+                      (TRIB && k0 < n0 + GBN && k0 + GBK > n0);
+#pragma unroll
+    for (int ks = 0; ks < GBK / 4; ++ks) {
+      const int k = ks * 4 + fk;
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 64 + i * 16 + fr;
+        a[i] = As[frag_off<A_KC>(r, k)];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = wn * 64 + j * 16 + fr;
+        b[j] = Bs[frag_off<B_KC>(c, k)];
+      }
+      if (mask) {
+        const int64_t gk = k0 + k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t gm = m0 + wm * 64 + i * 16 + fr;
+          if (gk >= kend || (TRIA && (TA ? gm > gk : gk > gm))) a[i] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t gn = n0 + wn * 64 + j * 16 + fr;
+          if (gk >= kend || (TRIB && (TB ? gk > gn : gn > gk))) b[j] = 0.0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const bool lower = p.uplo_c == VGPOSP_LOWER;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + fk + 4 * r;
+        if (row < p.m && col < p.n && (!lower || col <= row)) {
+          double* c = p.C + row * p.ldc + col;
+          double v = p.alpha * acc[i][j][r];
+          if (p.beta != 0.0) v += p.beta * *c;
+          *c = v;
+        }
+      }
+    }
+  }
+}
+
+int g_fast_gemm = 1;  // 0 forces the reference kernel (tests)
+
 static bool aligned16(const void* ptr, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(ptr) % 16 == 0) && (ld % 2 == 0);
 }
@@ -215,15 +404,37 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
                 double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
   GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b};
-  dim3 grid((unsigned)ceil_div(n, GBN), (unsigned)ceil_div(m, GBM));
   const int va = aligned16(A, lda), vb = aligned16(B, ldb);
+  const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
+  const bool tri_ok = (!tri_a && !tri_b) || (!transa && !transb && (tri_a != tri_b)) ||
+                      (transa && !transb && tri_a && tri_b);
+  if (va && vb && even && tri_ok && g_fast_gemm) {
+    const int tm = (int)ceil_div(m, GBM), tn = (int)ceil_div(n, GBN);
+    const int64_t nblk = (uplo_c == VGPOSP_LOWER) ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
+    const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
+    // algorithmic flops: a triangular operand halves the useful products
+    const double fl = 2.0 * (double)k * outs * ((tri_a && tri_b) ? (1.0 / 3.0) : (tri_a || tri_b) ? 0.5 : 1.0);
+    ProfScope ps("gemm_f64", stream, fl,
+                 8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    dim3 g1((unsigned)nblk);
+    if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true>), g1, dim3(256), 0, stream, p, tm, tn);
+    else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false>), g1, dim3(256), 0, stream, p, tm, tn);
+    else if (tri_b) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
+    else if (!transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
+    else if (!transa && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
+    else if (transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<true, false, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
+    else hipLaunchKernelGGL((gemm_glds_kernel<true, true, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
+    VG_LAUNCH_CHECK();
+    return 0;
+  }
+  dim3 grid((unsigned)ceil_div(n, GBN), (unsigned)ceil_div(m, GBM));
   const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
   ProfScope ps("gemm_f64", stream, 2.0 * (double)k * outs,
                8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
-  if (!transa && !transb) hipLaunchKernelGGL((gemm_f64_kernel<false, false>), grid, dim3(256), 0, stream, p, va, vb);
-  else if (!transa && transb) hipLaunchKernelGGL((gemm_f64_kernel<false, true>), grid, dim3(256), 0, stream, p, va, vb);
-  else if (transa && !transb) hipLaunchKernelGGL((gemm_f64_kernel<true, false>), grid, dim3(256), 0, stream, p, va, vb);
-  else hipLaunchKernelGGL((gemm_f64_kernel<true, true>), grid, dim3(256), 0, stream, p, va, vb);
+  if (!transa && !transb) hipLaunchKernelGGL((gemm_ref_kernel<false, false>), grid, dim3(256), 0, stream, p, va, vb);
+  else if (!transa && transb) hipLaunchKernelGGL((gemm_ref_kernel<false, true>), grid, dim3(256), 0, stream, p, va, vb);
+  else if (transa && !transb) hipLaunchKernelGGL((gemm_ref_kernel<true, false>), grid, dim3(256), 0, stream, p, va, vb);
+  else hipLaunchKernelGGL((gemm_ref_kernel<true, true>), grid, dim3(256), 0, stream, p, va, vb);
   VG_LAUNCH_CHECK();
   return 0;
 }

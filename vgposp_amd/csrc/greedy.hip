@@ -22,8 +22,8 @@
 namespace vgposp {
 
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
-              double* linv, hipStream_t stream);
-size_t potrf_ws_bytes();
+              void* ws, hipStream_t stream);
+size_t potrf_ws_bytes(int64_t n);
 
 constexpr int RC = 512;     // rows per chunk of the transposed mat-vec
 constexpr int CT = 256;     // columns per mat-vec workgroup
@@ -67,13 +67,13 @@ static GreedyWS greedy_layout(void* base, int64_t n, int kmax) {
   w.cnt = (long long*)take(8 * 8);
   w.fresh = (unsigned char*)take(n);
   w.selmask = (unsigned char*)take(n);
-  (void)take(potrf_ws_bytes());  // Linv scratch for the factorization (last)
+  (void)take(potrf_ws_bytes(n));  // factorization scratch (last)
   w.bytes = off;
   return w;
 }
 
-static double* greedy_linv(void* base, const GreedyWS& w) {
-  return reinterpret_cast<double*>(static_cast<char*>(base) + w.bytes - align_up(potrf_ws_bytes()));
+static void* greedy_fact_ws(void* base, const GreedyWS& w, int64_t n) {
+  return static_cast<char*>(base) + w.bytes - align_up(potrf_ws_bytes(n));
 }
 
 // Block-wide (value, index) arg-max for blockDim == 1024.  Result valid in all threads.
@@ -349,7 +349,7 @@ extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kma
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
                      n, lda, w);
   VG_LAUNCH_CHECK();
-  int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_linv(ws, w), s);
+  int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_fact_ws(ws, w, n), s);
   if (rc) return rc;
   // Q_ii = |M e_i|^2 -> part (reduced in the round-0 update)
   dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
