@@ -143,6 +143,17 @@ int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, in
                        size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * TF1 AdamOptimizer step on a device parameter vector (tf.train.AdamOptimizer in
+ * gp_functions.tf_train_gp_adam, gp_functions.py:179-182; variational_Gaussian_process_example.py
+ * :101-102).  g = grad_scale * grad (grad_scale = -1 maximises);  t = *step + 1 (device int64,
+ * incremented):  lr_t = lr sqrt(1 - b2^t) / (1 - b1^t);  m = b1 m + (1-b1) g;
+ * v = b2 v + (1-b2) g^2;  theta -= lr_t m / (sqrt(v) + eps).
+ * --------------------------------------------------------------------------------------------- */
+int vgposp_adam_update(double* theta, const double* grad, double* m, double* v, int64_t n,
+                       double lr, double beta1, double beta2, double eps, int64_t* step,
+                       double grad_scale, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Optional per-launch timing (no reference counterpart; the reference times with wall clocks,
  * placement_algorithm2.py:416-430).  When enabled, every launch of the library's named kernels
  * ("gemm_f64", "potrf_diag", "kernel_matrix", "greedy_trmv", "greedy_update", "greedy_select",

@@ -224,3 +224,76 @@ def calc_H(kind, X, y, noise, XEDGES, YEDGES, jitter=1e-6, scale=40.0):
             amp = scale * np.double((1 + j) / YEDGES)
             H[i, j] = gp_log_prob(kind, X, y, [amp], [ls], noise, jitter)[0]
     return H
+
+
+def vgp_optimal_posterior(kind, Z, X, y, amp, ls, noise, jitter=1e-6):
+    """Titsias optimal q(u) (TFP ~0.7 optimal_variational_posterior), kernel batch [B]."""
+    Kzz = kernel_matrix(kind, Z, Z, amp, ls)
+    Kzx = kernel_matrix(kind, Z, X, amp, ls)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    locs, scales = [], []
+    for b in range(Kzz.shape[0]):
+        M = Kzz.shape[-1]
+        Sinv = Kzz[b] + Kzx[b] @ Kzx[b].T / noise + jitter * np.eye(M)
+        L = np.linalg.cholesky(Sinv)
+        v = np.linalg.solve(L.T, np.linalg.solve(L, Kzx[b] @ y))
+        locs.append(Kzz[b] @ v / noise)
+        scales.append(np.linalg.solve(L, Kzz[b]))
+    return np.stack(locs), np.stack(scales)
+
+
+def vgp_variational_loss(kind, Z, Xb, yb, loc, scale, amp, ls, noise, kl_weight, jitter=1e-6,
+                         trace_adjoint=False):
+    """Negative ELBO averaged over the kernel batch (TFP ~0.7 variational_loss restated)."""
+    amp = np.atleast_1d(np.asarray(amp, dtype=np.float64))
+    ls = np.atleast_1d(np.asarray(ls, dtype=np.float64))
+    amp, ls = np.broadcast_arrays(amp, ls)
+    Kzz = kernel_matrix(kind, Z, Z, amp, ls)
+    Kzx = kernel_matrix(kind, Z, Xb, amp, ls)
+    yb = np.asarray(yb, dtype=np.float64).reshape(-1)
+    nb = yb.size
+    M = Kzz.shape[-1]
+    loc = np.asarray(loc).reshape(-1, M)
+    scale = np.asarray(scale).reshape(-1, M, M)
+    out = []
+    for b in range(Kzz.shape[0]):
+        lo = loc[b if loc.shape[0] > 1 else 0]
+        A = scale[b if scale.shape[0] > 1 else 0]
+        Lz = np.linalg.cholesky(Kzz[b] + jitter * np.eye(M))
+        kinv_loc = np.linalg.solve(Lz.T, np.linalg.solve(Lz, lo))
+        pred = Kzx[b].T @ kinv_loc
+        s2 = noise + jitter
+        obs_ll = np.sum(-0.5 * (yb - pred) ** 2 / s2 - 0.5 * np.log(2 * np.pi * s2))
+        G = np.linalg.solve(Lz, Kzx[b])
+        H = np.linalg.solve(Lz.T, G)
+        ktilde = nb * amp[b] ** 2 - np.sum(G ** 2)
+        AH = (A.T if trace_adjoint else A) @ H
+        trace_term = 0.5 * (ktilde + np.sum(AH ** 2)) / noise
+        Lp = np.linalg.cholesky(Kzz[b] + (noise + 1e-6) * np.eye(M))
+        P = np.linalg.solve(Lp, A)
+        q = np.linalg.solve(Lp, -lo)
+        kl = (np.sum(np.log(np.diag(Lp))) - np.linalg.slogdet(A)[1]
+              + 0.5 * (-M + np.sum(P ** 2) + np.sum(q ** 2)))
+        out.append(obs_ll - trace_term - kl_weight * kl)
+    return -np.mean(out)
+
+
+def vgp_predictive(kind, Xs, Z, loc, scale, amp, ls, pred_noise, jitter=1e-6):
+    """VGP posterior predictive mean [B, P] and covariance [B, P, P]."""
+    Kzz = kernel_matrix(kind, Z, Z, amp, ls)
+    Ksz = kernel_matrix(kind, Xs, Z, amp, ls)
+    Kss = kernel_matrix(kind, Xs, Xs, amp, ls)
+    M = Kzz.shape[-1]
+    loc = np.asarray(loc).reshape(-1, M)
+    scale = np.asarray(scale).reshape(-1, M, M)
+    means, covs = [], []
+    for b in range(Kzz.shape[0]):
+        lo = loc[b if loc.shape[0] > 1 else 0]
+        A = scale[b if scale.shape[0] > 1 else 0]
+        Lz = np.linalg.cholesky(Kzz[b] + jitter * np.eye(M))
+        T = np.linalg.solve(Lz.T, np.linalg.solve(Lz, Ksz[b].T))   # Kzz^-1 Kz*
+        means.append(T.T @ lo)
+        V = np.linalg.solve(Lz, Ksz[b].T)
+        U = A.T @ T
+        covs.append(Kss[b] - V.T @ V + U.T @ U + pred_noise * np.eye(Kss.shape[-1]))
+    return np.stack(means), np.stack(covs)

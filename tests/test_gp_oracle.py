@@ -1,0 +1,74 @@
+"""CPU checks of the TFP-semantics oracle (oracle/gp.py): LML against scikit-learn (exact match of
+the formula, jitter folded into alpha), gradients against finite differences, TF1 Adam."""
+import numpy as np
+import pytest
+
+from oracle import gp as ogp
+
+
+def test_lml_matches_sklearn():
+    from sklearn.gaussian_process import GaussianProcessRegressor
+    from sklearn.gaussian_process.kernels import RBF, ConstantKernel
+    from vgposp_amd.data_generation import grid_points, grid_observations
+    X = grid_points((5, 5, 5), jitter=0.05, seed=0)
+    y = grid_observations(X)
+    amp, ls, noise = 0.7444, 0.7444, 0.6931
+    lml = ogp.gp_log_prob("eq", X, y, amp, ls, noise)[0]
+    k = ConstantKernel(amp ** 2, "fixed") * RBF(ls, "fixed")
+    gpr = GaussianProcessRegressor(k, alpha=noise + 1e-6, optimizer=None, normalize_y=False).fit(X, y)
+    assert lml == pytest.approx(gpr.log_marginal_likelihood_value_, rel=1e-12)
+
+
+@pytest.mark.parametrize("kind", ogp.KERNELS)
+def test_lml_gradient_finite_difference(kind):
+    rng = np.random.default_rng(1)
+    X = rng.uniform(-2, 2, (40, 2))
+    y = np.sin(X).sum(1)
+    amp, ls, noise = np.array([0.9, 1.3]), np.array([0.5, 0.8]), 0.05
+    _, ga, gl, gn = ogp.gp_log_prob_and_grads(kind, X, y, amp, ls, noise)
+    h = 1e-6
+    for b in range(2):
+        e = np.eye(2)[b] * h
+        fa = (ogp.gp_log_prob(kind, X, y, amp + e, ls, noise) - ogp.gp_log_prob(kind, X, y, amp - e, ls, noise))[b] / (2 * h)
+        fl = (ogp.gp_log_prob(kind, X, y, amp, ls + e, noise) - ogp.gp_log_prob(kind, X, y, amp, ls - e, noise))[b] / (2 * h)
+        assert ga[b] == pytest.approx(fa, rel=1e-5, abs=1e-6)
+        assert gl[b] == pytest.approx(fl, rel=1e-5, abs=1e-6)
+    fn = (ogp.gp_log_prob(kind, X, y, amp, ls, noise + h) - ogp.gp_log_prob(kind, X, y, amp, ls, noise - h)) / (2 * h)
+    np.testing.assert_allclose(gn, fn, rtol=1e-5, atol=1e-6)
+
+
+def test_softplus_constraint_values():
+    # INIT 0.1 -> 0.7444, INIT 1e-6 -> 0.6931
+    assert ogp.constrain(0.1) == pytest.approx(0.744396660073571, rel=1e-12)
+    assert ogp.constrain(1e-6) == pytest.approx(0.6931476805599453, rel=1e-12)
+    assert ogp.constrain(ogp.invert_softplus(0.5)) == pytest.approx(0.5, rel=1e-14)
+
+
+def test_adam_tf1_first_step():
+    opt = ogp.AdamTF1(0.1)
+    th = opt.step(np.array([1.0, -2.0]), np.array([0.3, -4.0]))
+    # first TF1 Adam step moves every coordinate by ~lr * sign(g)
+    np.testing.assert_allclose(th, [1.0 - 0.1, -2.0 + 0.1], rtol=1e-6)
+
+
+def test_fit_increases_lml():
+    from vgposp_amd.data_generation import grid_points, grid_observations
+    X = grid_points((4, 4, 4), jitter=0.05, seed=0)
+    y = grid_observations(X)
+    lls, _ = ogp.fit_gp_adam("eq", X, y, [0.1, 0.1], [0.1, 0.1], 1e-6, 0.1, 30)
+    assert lls.shape == (31, 2)
+    assert np.all(lls[-1] > lls[0])
+
+
+def test_vgp_oracle_shapes_and_tightness():
+    """With Z = X the optimal variational posterior reproduces the exact posterior mean."""
+    rng = np.random.default_rng(2)
+    X = rng.uniform(-2, 2, (30, 1))
+    y = np.sin(3 * X[:, 0])
+    loc, scale = ogp.vgp_optimal_posterior("eq", X, X, y, 1.0, 0.5, 0.1)
+    assert loc.shape == (1, 30) and scale.shape == (1, 30, 30)
+    m_vgp, _ = ogp.vgp_predictive("eq", X, X, loc, scale, 1.0, 0.5, 0.0)
+    m_exact, _ = ogp.gprm_mean_cov("eq", X, X, y, 1.0, 0.5, 0.1, jitter=0.0)
+    np.testing.assert_allclose(m_vgp[0], m_exact[0], rtol=1e-4, atol=1e-6)
+    L = ogp.vgp_variational_loss("eq", X, X[:10], y[:10], loc, scale, 1.0, 0.5, 0.1, 10 / 30)
+    assert np.isfinite(L)

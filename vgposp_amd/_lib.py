@@ -69,6 +69,8 @@ SIGNATURES = {
     "vgposp_greedy_workspace_bytes": (_size, [_i64, _i32]),
     "vgposp_greedy_init": (_i32, [_c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p, _size,
                                   _c_void_p]),
+    "vgposp_adam_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64, _f64,
+                                  _f64, _f64, _c_void_p, _f64, _c_void_p]),
     "vgposp_prof_enable": (_i32, [_i32]),
     "vgposp_prof_query": (_i32, [ctypes.c_char_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64),
                                  ctypes.POINTER(_f64), ctypes.POINTER(_f64)]),

@@ -393,6 +393,31 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
   }
 }
 
+// y = alpha * A x + beta * y for a single output column (C = A B with n == 1): one wave per row,
+// HBM-bound (reads A once).  x is B's only column (stride ldb_x elements).
+__global__ __launch_bounds__(256) void gemv_rows_kernel(int64_t m, int64_t k, double alpha,
+                                                        const double* A, int64_t lda,
+                                                        const double* x, int64_t incx, double beta,
+                                                        double* y, int64_t incy) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= m) return;
+  const double* row = A + r * lda;
+  double s0 = 0.0, s1 = 0.0;
+  int64_t c = lane;
+  for (; c + 64 < k; c += 128) {
+    s0 += row[c] * x[c * incx];
+    s1 += row[c + 64] * x[(c + 64) * incx];
+  }
+  if (c < k) s0 += row[c] * x[c * incx];
+  const double s = wave_sum(s0 + s1);
+  if (lane == 0) {
+    double v = alpha * s;
+    if (beta != 0.0) v += beta * y[r * incy];
+    y[r * incy] = v;
+  }
+}
+
 int g_fast_gemm = 1;  // 0 forces the reference kernel (tests)
 
 static bool aligned16(const void* ptr, int64_t ld) {
@@ -403,11 +428,18 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
                 const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                 double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
+  if (n == 1 && !transa && !tri_a && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
+    ProfScope ps("gemv_f64", stream, 2.0 * (double)m * k, 8.0 * ((double)m * k + k + 2.0 * m));
+    hipLaunchKernelGGL(gemv_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, stream, m, k,
+                       alpha, A, lda, B, transb ? 1 : ldb, beta, C, ldc);
+    VG_LAUNCH_CHECK();
+    return 0;
+  }
   GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b};
   const int va = aligned16(A, lda), vb = aligned16(B, ldb);
   const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
   const bool tri_ok = (!tri_a && !tri_b) || (!transa && !transb && (tri_a != tri_b)) ||
-                      (transa && !transb && tri_a && tri_b);
+                      (!transa && transb && !tri_a && tri_b) || (transa && !transb && tri_a && tri_b);
   if (va && vb && even && tri_ok && g_fast_gemm) {
     const int tm = (int)ceil_div(m, GBM), tn = (int)ceil_div(n, GBN);
     const int64_t nblk = (uplo_c == VGPOSP_LOWER) ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
@@ -418,6 +450,7 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
                  8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
     dim3 g1((unsigned)nblk);
     if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true>), g1, dim3(256), 0, stream, p, tm, tn);
+    else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
     else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false>), g1, dim3(256), 0, stream, p, tm, tn);
     else if (tri_b) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
     else if (!transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, false>), g1, dim3(256), 0, stream, p, tm, tn);

@@ -41,13 +41,18 @@ __device__ long long g_stamps[8];
 constexpr int DP = NB + 1;  // LDS pitch (conflict-free column walks)
 constexpr int DIAG_THREADS = 1024;
 
+// Batched use (small matrices): workgroup b handles A + b * stride_a, info + b, diag_out + b * n
+// (linv must then be null).
 __global__ __launch_bounds__(DIAG_THREADS) void potrf_diag_kernel(double* A, int64_t lda, int jb,
                                                                   int64_t col0, int invert,
                                                                   double* linv, double* diag_out,
-                                                                  int* info) {
+                                                                  int* info, int64_t stride_a = 0) {
   extern __shared__ double L[];  // [NB][DP]; X (the inverse) lives transposed in the upper part
   __shared__ double rdiag[NB];   // 1 / L[r][r]
   const int t = threadIdx.x;
+  A += blockIdx.x * stride_a;
+  info += blockIdx.x;
+  if (diag_out) diag_out += (int64_t)blockIdx.x * jb;
   const int tx = t & 31, ty = t >> 5;
   for (int e = t; e < jb * jb; e += DIAG_THREADS) {
     const int r = e / jb, c = e % jb;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(DIAG_THREADS) void potrf_diag_kernel(double* A, int
     const int r = e / NB, c = e % NB;
     double x = 0.0;
     if (r < jb && c < jb && c <= r) x = (r == c) ? rdiag[c] : L[c * DP + r];
-    linv[e] = x;
+    if (linv) linv[e] = x;
     if (r < jb && c <= r) {
       A[(int64_t)r * lda + c] = invert ? x : L[r * DP + c];
     }
@@ -259,6 +264,20 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
   if (ws_bytes < potrf_ws_bytes(n)) {
     set_error("vgposp_potrf_lower: workspace %zu < %zu bytes", ws_bytes, potrf_ws_bytes(n));
     return VGPOSP_E_WS;
+  }
+  if (n <= NB && batch > 1) {
+    // one launch, one workgroup per matrix (e.g. the calc_H likelihood surface)
+    static bool attr_set = false;
+    if (!attr_set) {
+      VG_HIP(hipFuncSetAttribute((const void*)potrf_diag_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)diag_shmem()));
+      attr_set = true;
+    }
+    ProfScope ps("potrf_diag", s, batch * 2.0 * n * (double)n * n / 3.0, batch * 16.0 * n * (double)n);
+    hipLaunchKernelGGL(potrf_diag_kernel, dim3(batch), dim3(DIAG_THREADS), diag_shmem(), s, A, lda,
+                       (int)n, (int64_t)0, invert, (double*)nullptr, diag_out, info, stride);
+    VG_LAUNCH_CHECK();
+    return 0;
   }
   for (int b = 0; b < batch; ++b) {
     int rc = potrf_one(A + b * stride, n, lda, invert, diag_out ? diag_out + (int64_t)b * n : nullptr,
