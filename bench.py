@@ -175,6 +175,13 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = {name: _lib.prof_query(name) for name in
             ["kernel_matrix", "gemm_f64", "potrf_diag", "greedy_colsq", "greedy_trmv", "greedy_update"]}
+    # exact algorithmic bytes of the triangular mat-vec: rows >= a of the lower triangle of L^-1
+    # (the library only knows the full-triangle upper bound at launch time; a lives on device)
+    sel = [int(v) for v in g.selected.cpu()]
+    tri = lambda x: x * (x + 1) / 2.0  # noqa: E731
+    trmv_bytes = 8.0 * sum(tri(N) - tri(a) + 2 * N for a in sel[:-1]) * args.steps
+    ms_t, n_t, _, _ = prof["greedy_trmv"]
+    prof["greedy_trmv"] = (ms_t, n_t, 0.0, trmv_bytes)
     _lib.prof_enable(False)
     g.check()
     deterministic = bool(torch.equal(ref_sel, g.selected))

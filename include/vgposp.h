@@ -142,6 +142,26 @@ int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, in
                        int64_t* selected, double* sel_delta, int64_t* evals, void* ws,
                        size_t ws_bytes, void* stream);
 
+/* The two phases of vgposp_greedy_step, for candidate-sharded multi-GPU placement:
+ * every rank holds the factored Sigma (replicated init) and owns the candidate slab [c0, c1).
+ *   vgposp_greedy_update: rank-1 updates of nom / P_yy and fresh deltas for y in [c0, c1) only
+ *                         (the triangular mat-vec reads only the slab's columns of L^-1).
+ *   -> caller all-gathers the delta slabs into the full delta vector (vgposp_greedy_buffers)
+ *   vgposp_greedy_select: lazy-cache emulation over ALL candidates (identical on every rank) and
+ *                         the pivot row of the pick, written only by the rank whose slab owns it
+ *                         (zeros elsewhere)
+ *   -> caller sum-all-reduces the pivot buffer (2 + 2*kmax doubles) before the next update.
+ * With c0 = 0, c1 = n and no collectives this is exactly vgposp_greedy_step. */
+int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
+                         int64_t c0, int64_t c1, const int64_t* selected, void* ws,
+                         size_t ws_bytes, void* stream);
+int vgposp_greedy_select(int64_t n, int kmax, int round, int lazy, int64_t c0, int64_t c1,
+                         int64_t* selected, double* sel_delta, int64_t* evals, void* ws,
+                         size_t ws_bytes, void* stream);
+/* Device pointers into the workspace: the full delta vector [n] and the pivot buffer. */
+int vgposp_greedy_buffers(void* ws, int64_t n, int kmax, double** delta, double** piv,
+                          int64_t* piv_len);
+
 /* ---------------------------------------------------------------------------------------------
  * TF1 AdamOptimizer step on a device parameter vector (tf.train.AdamOptimizer in
  * gp_functions.tf_train_gp_adam, gp_functions.py:179-182; variational_Gaussian_process_example.py

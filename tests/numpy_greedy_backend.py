@@ -1,0 +1,105 @@
+"""TEST INFRASTRUCTURE: a numpy implementation of the libvgposp greedy phases
+(vgposp_greedy_init / _update / _select semantics) so the multi-rank orchestration of
+vgposp_amd.sharded_placement can be exercised with gloo on CPU.  Never used by the product."""
+import numpy as np
+import torch
+
+EPS = 1e-8
+
+
+def _keymax(vals, idx):
+    """(value desc, index asc) arg-max over candidate indices idx."""
+    if len(idx) == 0:
+        return -1
+    v = vals[idx]
+    best = np.max(v)
+    return int(idx[np.flatnonzero(v == best)[0]])
+
+
+class NumpyGreedyBackend:
+    def __init__(self, Sigma, kmax):
+        self.S = np.array(Sigma, dtype=np.float64)
+        self.n = self.S.shape[0]
+        self.kmax = kmax
+        self._delta = torch.zeros(self.n, dtype=torch.float64)
+        self._piv = torch.zeros(2 + 2 * kmax, dtype=torch.float64)
+
+    def init(self):
+        L = np.linalg.cholesky(self.S)
+        self.M = np.linalg.inv(L)
+        self.sdiag = np.diag(self.S).copy()
+        self.colsq = np.sum(self.M ** 2, axis=0)
+        n, k = self.n, self.kmax
+        self.nom = np.zeros(n)
+        self.prec = np.zeros(n)
+        self.W = np.zeros((k, n))
+        self.V = np.zeros((k, n))
+        self._delta.zero_()
+        self._piv.zero_()
+        self.cache = np.full(n, np.inf)
+        self.sel = np.zeros(n, dtype=bool)
+        self.selected = []
+        self.sel_delta = []
+
+    def update(self, rnd, c0, c1):
+        idx = np.arange(c0, c1)
+        if rnd == 0:
+            self.prec[idx] = self.colsq[idx]
+            self.nom[idx] = self.sdiag[idx]
+        else:
+            a, t1 = self.selected[rnd - 1], rnd - 1
+            piv = self._piv.numpy()
+            q = self.M[:, idx].T @ self.M[:, a]
+            s = self.S[idx, a].copy()
+            s -= piv[2:2 + t1] @ self.W[:t1][:, idx]
+            q -= piv[2 + t1:2 + 2 * t1] @ self.V[:t1][:, idx]
+            w = s / np.sqrt(piv[0]) if piv[0] > 0 else 0 * s
+            v = q / np.sqrt(piv[1]) if piv[1] > 0 else 0 * q
+            self.W[t1, idx] = w
+            self.V[t1, idx] = v
+            self.nom[idx] -= w * w
+            self.prec[idx] -= v * v
+        d = self._delta.numpy()
+        for i in idx:
+            if self.sel[i]:
+                continue
+            den = 1.0 / self.prec[i]
+            d[i] = 0.0 if (abs(den) < EPS or abs(self.nom[i]) < EPS) else self.nom[i] / den
+
+    def select(self, rnd, lazy, c0, c1):
+        d = self._delta.numpy()
+        cand = np.flatnonzero(~self.sel)
+        fy = _keymax(d, cand)
+        if not lazy:
+            y = fy
+        else:
+            fresh = np.zeros(self.n, dtype=bool)
+            for i in cand:
+                c = self.cache[i]
+                if c > d[fy] or (c == d[fy] and i < fy):
+                    self.cache[i] = d[i]
+                    fresh[i] = True
+            while True:
+                y = _keymax(self.cache, cand)
+                if fresh[y]:
+                    break
+                self.cache[y] = d[y]
+                fresh[y] = True
+        self.selected.append(y)
+        self.sel_delta.append(d[y])
+        self.sel[y] = True
+        p = self._piv.numpy()
+        p[:] = 0.0
+        if c0 <= y < c1:
+            p[0], p[1] = self.nom[y], self.prec[y]
+            p[2:2 + rnd] = self.W[:rnd, y]
+            p[2 + rnd:2 + 2 * rnd] = self.V[:rnd, y]
+
+    def delta(self):
+        return self._delta
+
+    def piv(self):
+        return self._piv
+
+    def result(self):
+        return [np.int64(s) for s in self.selected], np.array(self.sel_delta), None

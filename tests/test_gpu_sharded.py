@@ -1,0 +1,59 @@
+"""Candidate-sharded placement on the HIP path: 2 ranks (both on cuda:0, gloo with host staging)
+must reproduce the single-GPU / reference selections bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import gp as ogp
+from oracle import placement as op
+from tests.golden_io import placement_cases, placement_cov
+
+pytestmark = pytest.mark.gpu
+CASES = placement_cases()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _grid_cov():
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    X = grid_points((12, 10, 9), jitter=0.05, seed=9)
+    return ogp.kernel_matrix("eq", X, X, 1.0, 2 * grid_spacing((12, 10, 9)))[0] + 0.010001 * np.eye(len(X))
+
+
+def _worker(rank, world, port, out):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vgposp_amd.sharded_placement import placement_algorithm_2_sharded
+        res = {}
+        for name in ["spd40", "grid654", "grid8"]:
+            e = CASES[name]
+            res[name] = [int(a) for a in placement_algorithm_2_sharded(placement_cov(name, e), e["k"])]
+        res["grid1080"] = [int(a) for a in placement_algorithm_2_sharded(_grid_cov(), 12)]
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_ranks_on_gpu():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    exp_grid = op.placement_lazy_precision(_grid_cov(), 12)
+    for r in range(2):
+        for name in ["spd40", "grid654", "grid8"]:
+            assert out[r][name] == CASES[name]["alg2"], (r, name)
+        assert out[r]["grid1080"] == exp_grid

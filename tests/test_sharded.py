@@ -1,0 +1,77 @@
+"""Multi-rank candidate-sharded placement with world_size 2 / 3 on gloo (CPU):
+the orchestration (slab partition, delta all-gather, owner pivot all-reduce) must reproduce the
+reference's selections exactly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import placement as op
+from tests.golden_io import placement_cases, placement_cov
+from vgposp_amd.sharded_placement import slab_bounds
+
+CASES = placement_cases()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, names, lazy, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.numpy_greedy_backend import NumpyGreedyBackend
+        from vgposp_amd.sharded_placement import ShardedGreedyPlacement
+        res = {}
+        for name in names:
+            e = CASES[name]
+            cov = placement_cov(name, e)
+            sh = ShardedGreedyPlacement(NumpyGreedyBackend(cov, e["k"]))
+            A, _, _ = sh.run(e["k"], lazy=lazy)
+            res[name] = [int(a) for a in A]
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("lazy", [True, False])
+def test_sharded_matches_reference(world, lazy):
+    names = ["cov4x4", "spd40", "grid4", "grid654"] if lazy else ["cov4x4", "spd40", "grid4"]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), names, lazy, out), nprocs=world, join=True)
+    for r in range(world):
+        for name in names:
+            exp = CASES[name]["alg2" if lazy else "alg1"]
+            assert out[r][name] == exp, (r, name)
+
+
+def test_slab_bounds_balanced():
+    n = 65536
+    for world in (1, 2, 4, 8):
+        sl = slab_bounds(n, world)
+        assert sl[0][0] == 0 and sl[-1][1] == n
+        assert all(a <= b for a, b in sl)
+        work = [sum(n - c for c in range(a, b)) for a, b in sl] if n < 5000 else \
+            [(b - a) * n - (b * (b - 1) - a * (a - 1)) / 2 for a, b in sl]
+        assert max(work) / min(work) < 1.01
+    assert slab_bounds(3, 4)[-1][1] == 3
+
+
+def test_single_rank_numpy_backend_matches_oracle():
+    from tests.numpy_greedy_backend import NumpyGreedyBackend
+    from vgposp_amd.sharded_placement import ShardedGreedyPlacement
+    for name in ["grid5", "randcov11"]:
+        e = CASES[name]
+        sh = ShardedGreedyPlacement(NumpyGreedyBackend(placement_cov(name, e), e["k"]))
+        assert [int(a) for a in sh.run(e["k"])[0]] == e["alg2"]

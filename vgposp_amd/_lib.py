@@ -74,6 +74,12 @@ SIGNATURES = {
     "vgposp_prof_enable": (_i32, [_i32]),
     "vgposp_prof_query": (_i32, [ctypes.c_char_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64),
                                  ctypes.POINTER(_f64), ctypes.POINTER(_f64)]),
+    "vgposp_greedy_update": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i64, _i64, _c_void_p,
+                                    _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_select": (_i32, [_i64, _i32, _i32, _i32, _i64, _i64, _c_void_p, _c_void_p,
+                                    _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_buffers": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p),
+                                     ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),
     "vgposp_greedy_step": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                   _c_void_p, _c_void_p, _size, _c_void_p]),
 }

@@ -118,15 +118,16 @@ __global__ void greedy_extract_kernel(const double* M, int64_t n, int64_t lda,
 template <bool SQ>
 __global__ __launch_bounds__(CT) void greedy_trmv_kernel(const double* M, int64_t n, int64_t lda,
                                                          const int64_t* selected, int round,
-                                                         const double* xcol, double* part) {
-  const int64_t c0 = (int64_t)blockIdx.x * CT;
+                                                         const double* xcol, double* part,
+                                                         int64_t cbeg, int64_t cend) {
+  const int64_t c0 = cbeg + (int64_t)blockIdx.x * CT;
   const int64_t r0 = (int64_t)blockIdx.y * RC;
   const int64_t r1 = min(r0 + RC, n);
   if (c0 >= r1) return;  // tile strictly above the diagonal: never read by the reducer
   const int64_t a = SQ ? 0 : selected[round - 1];
   const int64_t c = c0 + threadIdx.x;
   double acc0 = 0.0, acc1 = 0.0;
-  if (c < n) {
+  if (c < cend) {
     int64_t r = max(max(r0, a), c);
     const double* p = M + r * lda + c;
     for (; r + 1 < r1; r += 2, p += 2 * lda) {
@@ -157,11 +158,9 @@ __device__ __forceinline__ double delta_of(double nom, double prec) {
 // Then delta for every unselected candidate and per-workgroup best fresh key.
 __global__ __launch_bounds__(CH) void greedy_update_kernel(const double* S, int64_t n, int64_t lda,
                                                            const int64_t* selected, int round,
-                                                           GreedyWS w) {
-  const int64_t i = (int64_t)blockIdx.x * CH + threadIdx.x;
-  double bv = -DBL_MAX;
-  long long bi = -1;
-  if (i < n) {
+                                                           GreedyWS w, int64_t cbeg, int64_t cend) {
+  const int64_t i = (cbeg / CH + (int64_t)blockIdx.x) * CH + threadIdx.x;
+  if (i >= cbeg && i < cend) {
     const int64_t nrc = (n + RC - 1) / RC;
     double q = 0.0;
     if (round == 0) {
@@ -185,12 +184,18 @@ __global__ __launch_bounds__(CH) void greedy_update_kernel(const double* S, int6
       w.nom[i] -= wy * wy;
       w.prec[i] -= vy * vy;
     }
-    if (!w.selmask[i]) {
-      const double d = delta_of(w.nom[i], w.prec[i]);
-      w.delta[i] = d;
-      bv = d;
-      bi = i;
-    }
+    if (!w.selmask[i]) w.delta[i] = delta_of(w.nom[i], w.prec[i]);
+  }
+}
+
+// Best fresh key F* per workgroup over all candidates (delta is complete on every rank here).
+__global__ __launch_bounds__(CH) void greedy_fresh_max_kernel(int64_t n, GreedyWS w) {
+  const int64_t i = (int64_t)blockIdx.x * CH + threadIdx.x;
+  double bv = -DBL_MAX;
+  long long bi = -1;
+  if (i < n && !w.selmask[i]) {
+    bv = w.delta[i];
+    bi = i;
   }
   block_keymax(bv, bi);
   if (threadIdx.x == 0) {
@@ -250,7 +255,8 @@ __global__ __launch_bounds__(CH) void greedy_refresh_kernel(int64_t n, GreedyWS 
 // One workgroup: the remaining re-score loop of placement_algorithm2.py:183-208, then selection.
 __global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round, int lazy,
                                                            int64_t* selected, double* sel_delta,
-                                                           int64_t* evals, GreedyWS w) {
+                                                           int64_t* evals, GreedyWS w,
+                                                           int64_t cbeg, int64_t cend) {
   __shared__ double cv[MAXCH];
   __shared__ long long ci[MAXCH];
   __shared__ long long ychosen;
@@ -305,19 +311,21 @@ __global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round,
     }
     return;
   }
-  // pivot data for the next update: nom_y, P_yy, W[0..round)[y], V[0..round)[y]
+  // pivot data for the next update: nom_y, P_yy, W[0..round)[y], V[0..round)[y].  Only the rank
+  // owning y's candidate slab holds them; the others write zeros (summed across ranks).
+  const bool own = y >= cbeg && y < cend;
   if (threadIdx.x == 0) {
     selected[round] = y;
     if (sel_delta) sel_delta[round] = w.delta[y];
-    if (evals) evals[round] = w.cnt[0] + loop_evals;
+    if (evals) evals[round] = lazy ? w.cnt[0] + loop_evals : n - round;
     w.cnt[0] = 0;
     w.selmask[y] = 1;
-    w.piv[0] = w.nom[y];
-    w.piv[1] = w.prec[y];
+    w.piv[0] = own ? w.nom[y] : 0.0;
+    w.piv[1] = own ? w.prec[y] : 0.0;
   }
   for (int t = threadIdx.x; t < round; t += blockDim.x) {
-    w.piv[2 + t] = w.W[(int64_t)t * n + y];
-    w.piv[2 + round + t] = w.V[(int64_t)t * n + y];
+    w.piv[2 + t] = own ? w.W[(int64_t)t * n + y] : 0.0;
+    w.piv[2 + round + t] = own ? w.V[(int64_t)t * n + y] : 0.0;
   }
 }
 
@@ -355,47 +363,75 @@ extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kma
   dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
   ProfScope ps("greedy_colsq", s, (double)n * (n + 1), 8.0 * (0.5 * (double)n * (n + 1) + (double)ceil_div(n, RC) * n));
   hipLaunchKernelGGL(greedy_trmv_kernel<true>, g, dim3(CT), 0, s, Sigma, n, lda, nullptr, 0,
-                     nullptr, w.part);
+                     nullptr, w.part, (int64_t)0, n);
   VG_LAUNCH_CHECK();
   return 0;
 }
 
-extern "C" int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
-                                  int lazy, int64_t* selected, double* sel_delta, int64_t* evals,
-                                  void* ws, size_t ws_bytes, void* stream) {
-  clear_error();
-  VG_CHECK_ARG(Sigma != nullptr, 1);
-  VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
-  VG_CHECK_ARG(lda >= n, 3);
-  VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
-  VG_CHECK_ARG(round >= 0 && round < kmax, 5);
-  VG_CHECK_ARG(selected != nullptr, 7);
-  VG_CHECK_ARG(ws != nullptr, 10);
-  GreedyWS w = greedy_layout(ws, n, kmax);
-  if (ws_bytes < w.bytes) {
-    set_error("vgposp_greedy_step: workspace %zu < %zu bytes", ws_bytes, w.bytes);
+static int greedy_check(const char* fn, const double* Sigma, int64_t n, int64_t lda, int kmax,
+                        int round, void* ws, size_t ws_bytes, GreedyWS* w) {
+  if (Sigma == nullptr) { set_error("%s: bad argument 1", fn); return -1; }
+  if (!(n >= 1 && n <= (int64_t)MAXCH * CH)) { set_error("%s: bad argument 2", fn); return -2; }
+  if (lda < n) { set_error("%s: bad argument 3", fn); return -3; }
+  if (!(kmax >= 1 && kmax <= n)) { set_error("%s: bad argument 4", fn); return -4; }
+  if (!(round >= 0 && round < kmax)) { set_error("%s: bad argument 5", fn); return -5; }
+  if (ws == nullptr) { set_error("%s: workspace is null", fn); return VGPOSP_E_WS; }
+  *w = greedy_layout(ws, n, kmax);
+  if (ws_bytes < w->bytes) {
+    set_error("%s: workspace %zu < %zu bytes", fn, ws_bytes, w->bytes);
     return VGPOSP_E_WS;
   }
+  return 0;
+}
+
+extern "C" int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda, int kmax,
+                                    int round, int64_t c0, int64_t c1, const int64_t* selected,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  GreedyWS w;
+  int rc = greedy_check(__func__, Sigma, n, lda, kmax, round, ws, ws_bytes, &w);
+  if (rc) return rc;
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= n, 6);
+  VG_CHECK_ARG(selected != nullptr || round == 0, 8);
   hipStream_t s = as_stream(stream);
-  const unsigned nch = (unsigned)ceil_div(n, CH);
+  if (c1 == c0) return 0;
   if (round > 0) {
     hipLaunchKernelGGL(greedy_extract_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
                        Sigma, n, lda, selected, round, w.xcol);
     VG_LAUNCH_CHECK();
-    dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
-    // algorithmic: the lower triangle of L^-1 in rows >= a (a is device-side: count the mean,
-    // n(n+1)/2 * (1 - E[a^2]/n^2) is not known on the host, so report the full triangle)
-    ProfScope ps("greedy_trmv", s, (double)n * (n + 1), 8.0 * (0.5 * (double)n * (n + 1) + 2.0 * n));
+    dim3 g((unsigned)ceil_div(c1 - c0, CT), (unsigned)ceil_div(n, RC));
+    // algorithmic: the lower triangle of L^-1 in rows >= a, columns [c0, c1) (a is device-side;
+    // bench.py recomputes the exact bytes from the selections)
+    ProfScope ps("greedy_trmv", s, 0.0, 8.0 * (0.5 * (double)n * (n + 1) + 2.0 * n));
     hipLaunchKernelGGL(greedy_trmv_kernel<false>, g, dim3(CT), 0, s, Sigma, n, lda, selected,
-                       round, w.xcol, w.part);
+                       round, w.xcol, w.part, c0, c1);
     VG_LAUNCH_CHECK();
   }
   {
-    ProfScope psu("greedy_update", s, 0.0, 8.0 * (double)n * (6 + 2.0 * round));
-    hipLaunchKernelGGL(greedy_update_kernel, dim3(nch), dim3(CH), 0, s, Sigma, n, lda, selected,
-                       round, w);
+    ProfScope psu("greedy_update", s, 0.0, 8.0 * (double)(c1 - c0) * (6 + 2.0 * round));
+    const int64_t b0 = c0 / CH, b1 = ceil_div(c1, CH);
+    // grid covers the CH-aligned blocks spanning [c0, c1); blockIdx is offset by b0
+    hipLaunchKernelGGL(greedy_update_kernel, dim3((unsigned)(b1 - b0)), dim3(CH), 0, s, Sigma, n,
+                       lda, selected, round, w, c0, c1);
     VG_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+extern "C" int vgposp_greedy_select(int64_t n, int kmax, int round, int lazy, int64_t c0,
+                                    int64_t c1, int64_t* selected, double* sel_delta,
+                                    int64_t* evals, void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  GreedyWS w;
+  double dummy = 0.0;
+  int rc = greedy_check(__func__, &dummy, n, n, kmax, round, ws, ws_bytes, &w);
+  if (rc) return rc;
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= n, 5);
+  VG_CHECK_ARG(selected != nullptr, 7);
+  hipStream_t s = as_stream(stream);
+  const unsigned nch = (unsigned)ceil_div(n, CH);
+  hipLaunchKernelGGL(greedy_fresh_max_kernel, dim3(nch), dim3(CH), 0, s, n, w);
+  VG_LAUNCH_CHECK();
   if (lazy) {
     ProfScope psr("greedy_refresh", s, 0.0, 8.0 * 3.0 * n);
     hipLaunchKernelGGL(greedy_refresh_kernel, dim3(nch), dim3(CH), 0, s, n, w);
@@ -403,7 +439,29 @@ extern "C" int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, i
   }
   ProfScope pss("greedy_select", s, 0.0, 0.0);
   hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(CH), 0, s, n, round, lazy, selected,
-                     sel_delta, evals, w);
+                     sel_delta, evals, w, c0, c1);
   VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
+                                  int lazy, int64_t* selected, double* sel_delta, int64_t* evals,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  int rc = vgposp_greedy_update(Sigma, n, lda, kmax, round, 0, n, selected, ws, ws_bytes, stream);
+  if (rc) return rc;
+  return vgposp_greedy_select(n, kmax, round, lazy, 0, n, selected, sel_delta, evals, ws, ws_bytes,
+                              stream);
+}
+
+extern "C" int vgposp_greedy_buffers(void* ws, int64_t n, int kmax, double** delta, double** piv,
+                                     int64_t* piv_len) {
+  clear_error();
+  VG_CHECK_ARG(ws != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(kmax >= 1, 3);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  if (delta) *delta = w.delta;
+  if (piv) *piv = w.piv;
+  if (piv_len) *piv_len = 2 + 2 * (int64_t)kmax;
   return 0;
 }

@@ -1,0 +1,140 @@
+"""Candidate-sharded greedy MI placement across GPUs, one process per GPU.
+
+The candidate set V is cut into R contiguous slabs (balanced by the work of the triangular
+mat-vec: column c of L^-1 has n - c stored rows).  Every rank holds the factored covariance
+(the O(N^3) init is replicated — "replicas only" for the factorization at N <= 65k) and, per round:
+
+  1. ``vgposp_greedy_update`` on its slab: W / V rank-1 rows, nom, P_yy and fresh deltas for the
+     slab's candidates only (the HBM-bound mat-vec reads only the slab's columns of L^-1);
+  2. ONE all-gather of the delta slabs (N x 8 bytes) so every rank holds all fresh deltas;
+  3. ``vgposp_greedy_select`` over ALL candidates — the reference's lazy-cache decisions
+     (placement_algorithm2.py:173-214) are re-run identically on every rank, so every rank picks
+     the same y* with no further exchange (the arg-max never needs a MAX-LOC collective);
+  4. ONE sum-all-reduce of the pivot row of y* (2 + 2 kmax doubles) that only its owner wrote.
+
+Nothing else crosses devices, and the selections are bit-identical to the single-GPU path (the
+per-column sums do not depend on the partition).  Collectives run on RCCL ("nccl" backend) over
+device tensors, or on gloo through host staging (the CPU tests).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._lib import call
+from .linalg import _p, _stream
+
+
+def slab_bounds(n, world, balance=True):
+    """Contiguous candidate slabs [c0, c1) per rank; balance=True equalises sum_c (n - c)."""
+    if not balance:
+        edges = [round(n * r / world) for r in range(world + 1)]
+    else:
+        total = n * (n + 1) / 2.0
+        edges = [0]
+        for r in range(1, world):
+            # solve c n - c^2/2 + c/2 = r/world * total for c
+            target = total * r / world
+            b = n + 0.5
+            c = b - np.sqrt(max(b * b - 2.0 * target, 0.0))
+            edges.append(int(min(max(round(c), edges[-1]), n)))
+        edges.append(n)
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
+class HipGreedyBackend:
+    """The per-rank device state: a GreedyPlacement plus tensor views of its delta / pivot."""
+
+    def __init__(self, Sigma, kmax, copy=False):
+        from .placement_algorithm2 import GreedyPlacement
+        self.g = GreedyPlacement(Sigma, kmax, copy=copy)
+        self.n = self.g.n
+        self.kmax = self.g.kmax
+        d, p, plen = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        call("vgposp_greedy_buffers", _p(self.g.ws), self.n, self.kmax, ctypes.byref(d),
+             ctypes.byref(p), ctypes.byref(plen))
+        base = self.g.ws.data_ptr()
+        self._delta = self.g.ws[d.value - base:d.value - base + 8 * self.n].view(torch.float64)
+        self._piv = self.g.ws[p.value - base:p.value - base + 8 * plen.value].view(torch.float64)
+
+    def init(self):
+        self.g.init()
+
+    def update(self, rnd, c0, c1):
+        g = self.g
+        call("vgposp_greedy_update", _p(g.S), g.n, g.S.stride(0), g.kmax, rnd, c0, c1,
+             _p(g.selected), _p(g.ws), g.ws.numel(), _stream())
+
+    def select(self, rnd, lazy, c0, c1):
+        g = self.g
+        call("vgposp_greedy_select", g.n, g.kmax, rnd, int(lazy), c0, c1, _p(g.selected),
+             _p(g.sel_delta), _p(g.evals), _p(g.ws), g.ws.numel(), _stream())
+        g.rounds = rnd + 1
+
+    def delta(self):
+        return self._delta
+
+    def piv(self):
+        return self._piv
+
+    def result(self):
+        return self.g.result()
+
+
+class ShardedGreedyPlacement:
+    def __init__(self, backend, group=None, balance=True):
+        self.b = backend
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.slabs = slab_bounds(backend.n, self.world, balance)
+        self.c0, self.c1 = self.slabs[self.rank]
+        self.S = max(c1 - c0 for c0, c1 in self.slabs)
+        dev = backend.delta().device
+        self.staging = (dist.is_initialized() and dist.get_backend(group) == "gloo"
+                        and dev.type != "cpu")
+        cdev = torch.device("cpu") if self.staging else dev
+        self.send = torch.zeros(self.S, dtype=torch.float64, device=cdev)
+        self.recv = torch.zeros(self.world * self.S, dtype=torch.float64, device=cdev)
+
+    def _allgather_delta(self):
+        d = self.b.delta()
+        self.send.zero_()
+        self.send[: self.c1 - self.c0].copy_(d[self.c0:self.c1])
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        else:
+            self.recv.copy_(self.send)
+        for r, (a, e) in enumerate(self.slabs):
+            if r != self.rank and e > a:
+                d[a:e].copy_(self.recv[r * self.S:r * self.S + (e - a)])
+
+    def _allreduce_piv(self):
+        if self.world == 1:
+            return
+        p = self.b.piv()
+        if self.staging:
+            h = p.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            p.copy_(h)
+        else:
+            dist.all_reduce(p, op=dist.ReduceOp.SUM, group=self.group)
+
+    def run(self, k, lazy=True):
+        self.b.init()
+        for rnd in range(k):
+            self.b.update(rnd, self.c0, self.c1)
+            self._allgather_delta()
+            self.b.select(rnd, lazy, self.c0, self.c1)
+            self._allreduce_piv()
+        return self.b.result()
+
+
+def placement_algorithm_2_sharded(cov_vv, k, group=None, lazy=True):
+    """placement_algorithm_2 with candidates sharded over the ranks of ``group`` (every rank
+    passes the same cov_vv and gets the same list)."""
+    sh = ShardedGreedyPlacement(HipGreedyBackend(cov_vv, k, copy=True), group)
+    return sh.run(k, lazy)[0]
