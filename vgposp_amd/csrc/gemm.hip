@@ -266,10 +266,16 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
   constexpr bool B_KC = TB;
   __shared__ double smem[STAGES * STAGE_ELEMS];
 
-  // XCD-aware bijective remap of the linear workgroup id.
+  // Tile order.  Uniform-K launches: XCD-aware bijective remap (each XCD walks a contiguous range
+  // of tiles, so neighbours share A rows / B columns in its L2).  A lower-triangular A (K range
+  // grows with the row tile) must NOT hand contiguous ranges to XCDs — one XCD would get every
+  // long tile — so it keeps the round-robin dispatch and walks row groups longest first.
   const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  int wg = bid;
+  if (!TRIA) {
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  }
   int ti, tj;
   if (p.uplo_c == VGPOSP_LOWER) {
     ti = tri_root(wg);
@@ -282,6 +288,7 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
     const int local = wg - g * per_group;
     ti = first + local % gsize;
     tj = local / gsize;
+    if (TRIA && !TA) ti = tiles_m - 1 - ti;  // longest K ranges first
   }
   const int64_t m0 = (int64_t)ti * GBM, n0 = (int64_t)tj * GBN;
 
