@@ -142,6 +142,22 @@ int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, in
                        int64_t* selected, double* sel_delta, int64_t* evals, void* ws,
                        size_t ws_bytes, void* stream);
 
+/* The TF-graph variant snippets_a2.sparse_placement_algorithm_2 (snippets_a2.py:679-822, with
+ * tf_nominator :138-213 and placement_algorithm2.sparse_argmax_cache_linear :24-50) differs only in
+ * three constants, which vgposp_greedy_init_ex stores in the workspace for the later rounds:
+ *   jitter      eps added to the diagonal of Sigma_AA and of Sigma_AbarAbar (snippets_a2.py:161-163:
+ *               1e-6; 0 for placement_algorithm_2).  The factorization is of Sigma + eps I and
+ *               denom_y = 1 / [(Sigma_SS + eps I)^-1]_yy - eps.
+ *   threshold   |nom| or |denom| < threshold -> delta = 0 (:480: 1e-7; 1e-8 for alg. 2)
+ *   cache_init  initial lazy-cache value (:690: INF = 1e8; +inf for alg. 2)
+ * vgposp_greedy_init(...) == vgposp_greedy_init_ex(..., 0, 1e-8, +inf, ...).
+ * vgposp_greedy_cache returns the device pointer of the lazy cache [n] (delta_cached): the
+ * per-round snapshot delta_cached_iters[:, r] of the TF variant is a copy of it after round r. */
+int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int kmax, double jitter,
+                          double threshold, double cache_init, int* info, void* ws,
+                          size_t ws_bytes, void* stream);
+int vgposp_greedy_cache(void* ws, int64_t n, int kmax, double** cache);
+
 /* The two phases of vgposp_greedy_step, for candidate-sharded multi-GPU placement:
  * every rank holds the factored Sigma (replicated init) and owns the candidate slab [c0, c1).
  *   vgposp_greedy_update: rank-1 updates of nom / P_yy and fresh deltas for y in [c0, c1) only

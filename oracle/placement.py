@@ -141,10 +141,12 @@ def placement_algorithm_1(cov_vv, k):
 # ---------------------------------------------------------------------------------------------
 # Precision-matrix restatement (same decisions, O(N^3) once + O(kN^2)): pinned against the above.
 # ---------------------------------------------------------------------------------------------
-def all_deltas(cov_vv, A):
+def all_deltas(cov_vv, A, jitter=0.0, thr=DELTA_EPS):
     """delta_y(A) for every y (selected entries -> nan), via
-    nom_y   = sigma_yy - Sigma_yA Sigma_AA^-1 Sigma_Ay
-    denom_y = 1 / [(Sigma_SS)^-1]_yy,   S = V \\ A  (conditional variance given S \\ {y})."""
+    nom_y   = sigma_yy - Sigma_yA (Sigma_AA + eps I)^-1 Sigma_Ay
+    denom_y = 1 / [(Sigma_SS + eps I)^-1]_yy - eps,   S = V \\ A
+    (the conditional variance of y given S \\ {y} with eps on that block's diagonal; eps = 0 for
+    placement_algorithm2, 1e-6 for the TF variant)."""
     cov = np.asarray(cov_vv, dtype=np.float64)
     N = cov.shape[0]
     A = [int(a) for a in A]
@@ -153,7 +155,7 @@ def all_deltas(cov_vv, A):
     den = np.full(N, np.nan)
     diag = np.diag(cov)
     if A:
-        LA = np.linalg.cholesky(cov[np.ix_(A, A)])
+        LA = np.linalg.cholesky(cov[np.ix_(A, A)] + jitter * np.eye(len(A)))
         W = np.linalg.solve(LA, cov[A, :])
         nom[S] = diag[S] - np.sum(W[:, S] ** 2, axis=0)
     else:
@@ -161,10 +163,10 @@ def all_deltas(cov_vv, A):
     if len(S) == 1:
         den[S] = diag[S]
     elif len(S) > 1:
-        P = np.linalg.inv(cov[np.ix_(S, S)])
-        den[S] = 1.0 / np.diag(P)
+        P = np.linalg.inv(cov[np.ix_(S, S)] + jitter * np.eye(len(S)))
+        den[S] = 1.0 / np.diag(P) - jitter
     delta = np.full(N, np.nan)
-    ok = (np.abs(nom[S]) >= DELTA_EPS) & (np.abs(den[S]) >= DELTA_EPS)
+    ok = (np.abs(nom[S]) >= thr) & (np.abs(den[S]) >= thr)
     d = np.zeros(len(S))
     d[ok] = nom[S][ok] / den[S][ok]
     delta[S] = d
@@ -192,15 +194,19 @@ def lazy_select(cache, fresh_delta, selected):
         evaluated.append(y_st)
 
 
-def placement_lazy_precision(cov_vv, k, lazy=True):
-    """Same selections as placement_algorithm_2 (lazy=True) / _1 (lazy=False) up to rounding."""
+def placement_lazy_precision(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, cache_init=np.inf,
+                             snapshots=None):
+    """Same selections as placement_algorithm_2 (lazy=True) / _1 (lazy=False) up to rounding;
+    with (jitter, thr, cache_init) = (1e-6, 1e-7, 1e8) and ``snapshots`` (a list receiving the
+    cache after each round, the selected entry then zeroed) it restates the TF variant
+    ``sparse_placement_algorithm_2`` below."""
     cov = np.asarray(cov_vv, dtype=np.float64)
     N = cov.shape[0]
-    cache = np.full(N, np.inf)
+    cache = np.full(N, float(cache_init))
     selected = np.zeros(N, dtype=bool)
     A = []
     for _ in range(k):
-        delta, _, _ = all_deltas(cov, A)
+        delta, _, _ = all_deltas(cov, A, jitter, thr)
         if lazy:
             y, _ = lazy_select(cache, delta, selected)
         else:
@@ -208,4 +214,84 @@ def placement_lazy_precision(cov_vv, k, lazy=True):
             y = int(np.argmax(d))
         A.append(int(y))
         selected[y] = True
+        if snapshots is not None:
+            snapshots.append(cache.copy())
+            cache[y] = 0.0
     return A
+
+
+# ---------------------------------------------------------------------------------------------
+# The TF-graph variant: snippets_a2.sparse_placement_algorithm_2 (snippets_a2.py:679-822).
+# TensorFlow is absent, so this is a restatement from the source (parity unpinned by execution);
+# with TF_JITTER = 0, TF_SMALL = 1e-8 and TF_INF = inf it reduces to placement_algorithm_2 above,
+# which IS pinned by the reference's own outputs.
+# ---------------------------------------------------------------------------------------------
+TF_JITTER = 1e-6   # snippets_a2.py:161-163  (diag of cov_AA += 1e-6 before pinv)
+TF_SMALL = 1e-7    # snippets_a2.py:480  (if_denom_is_near_zero)
+TF_INF = 1e8       # snippets_a2.py:690
+
+
+def tf_pinv(a):
+    """tfp.math.pinv with its default rcond = 10 * max(rows, cols) * eps(float64)."""
+    return np.linalg.pinv(a, rcond=10.0 * max(a.shape) * np.finfo(np.float64).eps)
+
+
+def tf_nominator(y, A, cov_vv, jitter=TF_JITTER):
+    """snippets_a2.py:138-213 — sigma_yy - Sigma_yA pinv(Sigma_AA + eps I) Sigma_Ay, A \\ {y}."""
+    A_ = sorted(int(a) for a in set(A) - {int(y)})   # tf.sets keep their values sorted
+    sigm_yy = cov_vv[y, y]
+    if not A_:
+        return sigm_yy
+    cov_yA = cov_vv[y, A_]
+    cov_AA = cov_vv[np.ix_(A_, A_)].copy()
+    cov_AA[np.diag_indices(len(A_))] += jitter
+    cov_Ay = cov_vv[A_, y]
+    mul1 = np.tensordot(cov_yA, tf_pinv(cov_AA), [[0], [0]])
+    return sigm_yy - np.tensordot(mul1, cov_Ay, [[0], [0]])
+
+
+def tf_denominator(y, A_hat, cov_vv, jitter=TF_JITTER):
+    """snippets_a2.py:215-217."""
+    return tf_nominator(y, set(A_hat) - {int(y)}, cov_vv, jitter)
+
+
+def sparse_argmax_cache_linear(cache, A, N):
+    """placement_algorithm2.py:24-50 — max over V \\ A (ascending), first (lowest) index of ties."""
+    Aset = set(A)
+    cand = np.array([v for v in range(N) if v not in Aset], dtype=np.int64)
+    vals = cache[cand]
+    return int(cand[np.flatnonzero(vals == vals.max())[0]])
+
+
+def sparse_placement_algorithm_2(cov_vv, k, COVER_spatial, trace=None, jitter=TF_JITTER,
+                                 small=TF_SMALL, inf=TF_INF):
+    """snippets_a2.py:679-822.  Returns (A sorted as the tf.sets SparseTensor values, len(A),
+    delta_cached_iters [N, k], A_selection_and_delta [k, 2]).  The keyword constants exist so
+    tests can set them to placement_algorithm_2's (0, 1e-8, inf) and pin against its goldens."""
+    cov = np.asarray(cov_vv, dtype=np.float64)
+    N = cov.shape[0]
+    if N != int(np.prod(COVER_spatial[:3])):                       # :692 tf.Assert
+        raise ValueError(f"N = {N} != prod(COVER_spatial) = {int(np.prod(COVER_spatial[:3]))}")
+    A, A_bar = [], list(range(N))
+    cache = np.full(N, float(inf))                                     # :708
+    dci = np.zeros((N, k))
+    sel = np.zeros((k, 2))
+    for r in range(k):                                             # body_A :717-802
+        uptodate = np.zeros(N, dtype=bool)                         # :722
+        while True:                                                # while_true_outside / _inside
+            y = sparse_argmax_cache_linear(cache, A, N)
+            if uptodate[y]:
+                break
+            nom = tf_nominator(y, A, cov, jitter)
+            denom = tf_denominator(y, A_bar, cov, jitter)
+            near = abs(denom) < small or abs(nom) < small
+            cache[y] = 0.0 if near else nom / denom                 # then_update_delta_y
+            uptodate[y] = True
+            if trace is not None:
+                trace.append((y, float(cache[y])))
+        A.append(y)                                                # append_to_A_remove_from_A_bar
+        A_bar.remove(y)
+        sel[r] = (y, cache[y])                                     # :767-768
+        dci[:, r] = cache                                          # :778
+        cache[y] = 0.0                                             # :796
+    return sorted(A), len(A), dci, sel

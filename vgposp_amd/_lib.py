@@ -69,6 +69,9 @@ SIGNATURES = {
     "vgposp_greedy_workspace_bytes": (_size, [_i64, _i32]),
     "vgposp_greedy_init": (_i32, [_c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p, _size,
                                   _c_void_p]),
+    "vgposp_greedy_init_ex": (_i32, [_c_void_p, _i64, _i64, _i32, _f64, _f64, _f64, _c_void_p,
+                                     _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_cache": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p)]),
     "vgposp_adam_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64, _f64,
                                   _f64, _f64, _c_void_p, _f64, _c_void_p]),
     "vgposp_prof_enable": (_i32, [_i32]),

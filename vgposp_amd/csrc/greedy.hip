@@ -31,8 +31,14 @@ constexpr int CH = 1024;    // candidates per chunk / per update workgroup
 constexpr int MAXCH = 2048; // chunks held in LDS by the select kernel -> n <= 2^21
 constexpr double DELTA_EPS = 1e-8;  // placement_algorithm2.py:198
 
+// Variant parameters, written by vgposp_greedy_init_ex into the workspace (device memory) so the
+// per-round entry points keep their signatures:
+//   prm[0] jitter  eps added to the diagonal of Sigma_AA and Sigma_AbarAbar (0 for
+//                  placement_algorithm2.py; 1e-6 for snippets_a2.tf_nominator :161-163)
+//   prm[1] thr     |nom| or |denom| below thr -> delta = 0 (1e-8 at :198; 1e-7 at snippets_a2 :480)
+//   prm[2] cinit   initial lazy-cache value (+inf at :164; INF = 1e8 at snippets_a2 :690)
 struct GreedyWS {
-  double *sdiag, *nom, *prec, *delta, *cache, *W, *V, *part, *xcol, *piv, *fval, *cval;
+  double *prm, *sdiag, *nom, *prec, *delta, *cache, *W, *V, *part, *xcol, *piv, *fval, *cval;
   long long *fidx, *cidx, *cnt;
   unsigned char *fresh, *selmask;
   size_t bytes;
@@ -50,6 +56,7 @@ static GreedyWS greedy_layout(void* base, int64_t n, int kmax) {
     off += align_up(bytes);
     return r;
   };
+  w.prm = (double*)take(8 * 8);
   w.sdiag = (double*)take(n * 8);
   w.nom = (double*)take(n * 8);
   w.prec = (double*)take(n * 8);
@@ -94,14 +101,25 @@ __device__ __forceinline__ void block_keymax(double& v, long long& i) {
   wave_keymax(v, i);  // every wave reduces the same 16 entries
 }
 
-__global__ void greedy_init_kernel(const double* S, int64_t n, int64_t lda, GreedyWS w) {
+// Saves diag(Sigma), shifts the diagonal by the jitter (the factorization is of Sigma + eps I:
+// the inverse of Sigma_SS + eps I is the Schur complement of the A block of (Sigma + eps I)^-1),
+// and fills the cache with its initial value.
+__global__ void greedy_init_kernel(double* S, int64_t n, int64_t lda, double jitter, double thr,
+                                   double cinit, GreedyWS w) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    w.sdiag[i] = S[i * lda + i];
-    w.cache[i] = __builtin_huge_val();  // INF = 1e1000 (placement_algorithm2.py:164)
+    const double d = S[i * lda + i];
+    w.sdiag[i] = d;
+    if (jitter != 0.0) S[i * lda + i] = d + jitter;
+    w.cache[i] = cinit;
     w.selmask[i] = 0;
   }
   if (i < 8) w.cnt[i] = 0;
+  if (i == 0) {
+    w.prm[0] = jitter;
+    w.prm[1] = thr;
+    w.prm[2] = cinit;
+  }
 }
 
 // x = M e_a restricted to rows >= a (the selected column of L^-1), a = selected[round-1].
@@ -148,9 +166,11 @@ __global__ __launch_bounds__(CT) void greedy_trmv_kernel(const double* M, int64_
   }
 }
 
-__device__ __forceinline__ double delta_of(double nom, double prec) {
-  const double den = 1.0 / prec;
-  if (fabs(den) < DELTA_EPS || fabs(nom) < DELTA_EPS) return 0.0;  // :198
+// denom = conditional variance of y given V \ (A u {y}) with eps on that block's diagonal:
+// 1 / [(Sigma_SS + eps I)^-1]_yy - eps (Sherman-Morrison on the y entry of the jitter).
+__device__ __forceinline__ double delta_of(double nom, double prec, double eps, double thr) {
+  const double den = 1.0 / prec - eps;
+  if (fabs(den) < thr || fabs(nom) < thr) return 0.0;  // :198 / snippets_a2.py:440-487
   return nom / den;
 }
 
@@ -160,6 +180,7 @@ __global__ __launch_bounds__(CH) void greedy_update_kernel(const double* S, int6
                                                            const int64_t* selected, int round,
                                                            GreedyWS w, int64_t cbeg, int64_t cend) {
   const int64_t i = (cbeg / CH + (int64_t)blockIdx.x) * CH + threadIdx.x;
+  const double eps = w.prm[0], thr = w.prm[1];
   if (i >= cbeg && i < cend) {
     const int64_t nrc = (n + RC - 1) / RC;
     double q = 0.0;
@@ -176,7 +197,8 @@ __global__ __launch_bounds__(CH) void greedy_update_kernel(const double* S, int6
         s -= w.piv[2 + t] * w.W[(int64_t)t * n + i];
         q -= w.piv[2 + t1 + t] * w.V[(int64_t)t * n + i];
       }
-      const double noma = w.piv[0], preca = w.piv[1];
+      // pivot of the Cholesky of Sigma_AA + eps I: nom_a + eps
+      const double noma = w.piv[0] + eps, preca = w.piv[1];
       const double wy = noma > 0.0 ? s / sqrt(noma) : 0.0;
       const double vy = preca > 0.0 ? q / sqrt(preca) : 0.0;
       w.W[(int64_t)t1 * n + i] = wy;
@@ -184,7 +206,7 @@ __global__ __launch_bounds__(CH) void greedy_update_kernel(const double* S, int6
       w.nom[i] -= wy * wy;
       w.prec[i] -= vy * vy;
     }
-    if (!w.selmask[i]) w.delta[i] = delta_of(w.nom[i], w.prec[i]);
+    if (!w.selmask[i]) w.delta[i] = delta_of(w.nom[i], w.prec[i], eps, thr);
   }
 }
 
@@ -338,15 +360,19 @@ extern "C" size_t vgposp_greedy_workspace_bytes(int64_t n, int kmax) {
   return greedy_layout(nullptr, n, kmax).bytes;
 }
 
-extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kmax, int* info,
-                                  void* ws, size_t ws_bytes, void* stream) {
+extern "C" int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int kmax,
+                                     double jitter, double threshold, double cache_init, int* info,
+                                     void* ws, size_t ws_bytes, void* stream) {
   clear_error();
   VG_CHECK_ARG(Sigma != nullptr, 1);
   VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
   VG_CHECK_ARG(lda >= n, 3);
   VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
-  VG_CHECK_ARG(info != nullptr, 5);
-  VG_CHECK_ARG(ws != nullptr, 6);
+  VG_CHECK_ARG(jitter >= 0.0 && jitter < 1e300, 5);
+  VG_CHECK_ARG(threshold >= 0.0, 6);
+  VG_CHECK_ARG(cache_init == cache_init, 7);
+  VG_CHECK_ARG(info != nullptr, 8);
+  VG_CHECK_ARG(ws != nullptr, 9);
   GreedyWS w = greedy_layout(ws, n, kmax);
   if (ws_bytes < w.bytes) {
     set_error("vgposp_greedy_init: workspace %zu < %zu bytes", ws_bytes, w.bytes);
@@ -355,7 +381,7 @@ extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kma
   hipStream_t s = as_stream(stream);
   VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
-                     n, lda, w);
+                     n, lda, jitter, threshold, cache_init, w);
   VG_LAUNCH_CHECK();
   int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_fact_ws(ws, w, n), s);
   if (rc) return rc;
@@ -366,6 +392,15 @@ extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kma
                      nullptr, w.part, (int64_t)0, n);
   VG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int vgposp_greedy_init(double* Sigma, int64_t n, int64_t lda, int kmax, int* info,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(info != nullptr, 5);  // argument numbers of this signature
+  VG_CHECK_ARG(ws != nullptr, 6);
+  return vgposp_greedy_init_ex(Sigma, n, lda, kmax, 0.0, DELTA_EPS, __builtin_huge_val(), info,
+                               ws, ws_bytes, stream);
 }
 
 static int greedy_check(const char* fn, const double* Sigma, int64_t n, int64_t lda, int kmax,
@@ -463,5 +498,15 @@ extern "C" int vgposp_greedy_buffers(void* ws, int64_t n, int kmax, double** del
   if (delta) *delta = w.delta;
   if (piv) *piv = w.piv;
   if (piv_len) *piv_len = 2 + 2 * (int64_t)kmax;
+  return 0;
+}
+
+extern "C" int vgposp_greedy_cache(void* ws, int64_t n, int kmax, double** cache) {
+  clear_error();
+  VG_CHECK_ARG(ws != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(kmax >= 1, 3);
+  VG_CHECK_ARG(cache != nullptr, 4);
+  *cache = greedy_layout(ws, n, kmax).cache;
   return 0;
 }

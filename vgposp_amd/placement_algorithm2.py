@@ -19,6 +19,8 @@ host round trip between selections).
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -35,7 +37,8 @@ class GreedyPlacement:
     nominators read.  Pass ``copy=True`` to work on a private copy.
     """
 
-    def __init__(self, Sigma, kmax, copy=False):
+    def __init__(self, Sigma, kmax, copy=False, jitter=0.0, threshold=1e-8,
+                 cache_init=float("inf")):
         S = linalg.as_device(Sigma)
         if S.dim() != 2 or S.shape[0] != S.shape[1]:
             raise ValueError("cov_vv must be a square matrix")
@@ -51,12 +54,22 @@ class GreedyPlacement:
         self.sel_delta = torch.zeros(self.kmax, dtype=torch.float64, device=dev)
         self.evals = torch.zeros(self.kmax, dtype=torch.int64, device=dev)
         self.rounds = 0
+        # (jitter, |nom|/|denom| threshold, initial cache): (0, 1e-8, inf) is placement_algorithm2;
+        # (1e-6, 1e-7, 1e8) is the TF variant snippets_a2.sparse_placement_algorithm_2
+        self.params = (float(jitter), float(threshold), float(cache_init))
 
     def init(self):
-        call("vgposp_greedy_init", _p(self.S), self.n, self.S.stride(0), self.kmax, _p(self.info),
-             _p(self.ws), self.ws.numel(), _stream())
+        call("vgposp_greedy_init_ex", _p(self.S), self.n, self.S.stride(0), self.kmax,
+             *self.params, _p(self.info), _p(self.ws), self.ws.numel(), _stream())
         self.rounds = 0
         return self
+
+    def cache(self):
+        """Device view of the lazy cache (delta_cached) [n] inside the workspace."""
+        c = ctypes.c_void_p()
+        call("vgposp_greedy_cache", _p(self.ws), self.n, self.kmax, ctypes.byref(c))
+        off = c.value - self.ws.data_ptr()
+        return self.ws[off:off + 8 * self.n].view(torch.float64)
 
     def check(self):
         linalg.check_info(self.info)
