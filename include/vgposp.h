@@ -80,6 +80,35 @@ int vgposp_gemm(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
                 const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                 double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, void* stream);
 
+/* Split-K form of vgposp_gemm for few output tiles and a long K (e.g. the VGP's
+ * Kzx Kzx^T with M = 512 inducing points and K = N = 262,144 observations: 10 lower tiles).  Each
+ * of `splits` K-ranges writes alpha * partial into ws ([splits][m][n]); a second kernel sums them
+ * in a fixed order and adds beta * C, so results are deterministic.  splits <= 0 chooses a count
+ * (about 512 workgroups, >= 512-deep ranges).  Falls back to vgposp_gemm's kernels (no split) for
+ * operands the MFMA path does not take. */
+size_t vgposp_gemm_splitk_workspace_bytes(int64_t m, int64_t n, int64_t k, int uplo_c, int splits);
+int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                       const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                       double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int splits,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Vector-Jacobian product of kernel assembly: the reverse pass TF autodiff runs through
+ * kernel.matrix when the reference trains a VGP (variational_Gaussian_process_example.py:95-102,
+ * AdamOptimizer.minimize over amplitude, length_scale, inducing_index_points).  For one kernel
+ * (amp, ls: device [1]) and Kbar [n1 x n2] (ld ldk) plus an optional rank-1 term u w^T
+ * (u: [n1], w: [n2], both NULL or both set):
+ *     grad[0] = sum_ij Kbar_ij dK_ij/damp,   grad[1] = sum_ij Kbar_ij dK_ij/dls,
+ *     X1bar[i][:] = sum_j Kbar_ij dK_ij/dX1[i][:]    (X1bar [n1 x d] or NULL)
+ * K is recomputed on the fly (one HBM pass over Kbar).  Deterministic (fixed-order reduction).
+ * For a symmetric use (K(Z, Z)) pass Kbar + Kbar^T and halve grad.
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_kernel_vjp_workspace_bytes(int64_t n1, int64_t n2, int d);
+int vgposp_kernel_vjp(int kind, const double* X1, int64_t n1, const double* X2, int64_t n2, int d,
+                      const double* amp, const double* ls, const double* Kbar, int64_t ldk,
+                      const double* u, const double* w, double* grad, double* X1bar, void* ws,
+                      size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Blocked right-looking Cholesky, lower, in place.  Replaces tf.linalg.cholesky inside
  * tfd.GaussianProcess.log_prob / GPRM / VGP (gp_functions.py:166-172, main.py:105,

@@ -297,3 +297,144 @@ def vgp_predictive(kind, Xs, Z, loc, scale, amp, ls, pred_noise, jitter=1e-6):
         U = A.T @ T
         covs.append(Kss[b] - V.T @ V + U.T @ U + pred_noise * np.eye(Kss.shape[-1]))
     return np.stack(means), np.stack(covs)
+
+
+# ---------------------------------------------------------------------------------------------
+# VGP training objective of variational_Gaussian_process_example.py:51-102: the minibatch
+# variational_loss of a VGP whose q(u) is optimal_variational_posterior over the FULL data,
+# differentiated w.r.t. (amp, ls, noise, Z).  The analytic gradient below is checked against
+# central finite differences of vgp_training_loss in tests/test_gp_oracle.py.
+# ---------------------------------------------------------------------------------------------
+def vgp_training_loss(kind, Z, X, y, Xb, yb, amp, ls, noise, kl_weight, jitter=1e-6,
+                      trace_adjoint=False):
+    loc, scale = vgp_optimal_posterior(kind, Z, X, y, amp, ls, noise, jitter)
+    return vgp_variational_loss(kind, Z, Xb, yb, loc, scale, amp, ls, noise, kl_weight, jitter,
+                                trace_adjoint)
+
+
+def kernel_vjp(kind, X1, X2, amp, ls, Kbar):
+    """sum_ij Kbar_ij dK_ij/d(amp, ls, X1_i): returns (g_amp, g_ls, X1bar [n1, d])."""
+    X1 = np.asarray(X1, dtype=np.float64).reshape(len(X1), -1)
+    X2 = np.asarray(X2, dtype=np.float64).reshape(len(X2), -1)
+    K = kernel_matrix(kind, X1, X2, amp, ls)[0]
+    dA, dL = kernel_matrix_grads(kind, X1, X2, amp, ls)
+    diff = X1[:, None, :] - X2[None, :, :]
+    r = np.sqrt(np.sum(diff ** 2, axis=-1)) / ls
+    a2 = amp ** 2
+    # dK/dx1 = a^2 g(r) (x1 - x2) / ls^2 with g = f'(r) / r
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if kind == "eq":
+            g = -K / a2
+        elif kind == "matern12":
+            g = np.where(r > 0, -np.exp(-r) / r, 0.0)
+        elif kind == "matern32":
+            g = -3.0 * np.exp(-np.sqrt(3.0) * r)
+        elif kind == "matern52":
+            s = np.sqrt(5.0) * r
+            g = -(5.0 / 3.0) * (1.0 + s) * np.exp(-s)
+    coef = Kbar * a2 * g / ls ** 2
+    X1bar = np.einsum("ij,ijk->ik", coef, diff)
+    return np.sum(Kbar * dA[0]), np.sum(Kbar * dL[0]), X1bar
+
+
+def _chol_backward(Li, Lbar):
+    """Symmetric adjoint of A = L L^T given Lbar (lower): sym(L^-T Phi(L^T Lbar) L^-1)."""
+    L = np.linalg.inv(Li)
+    P = np.tril(L.T @ Lbar)
+    P[np.diag_indices_from(P)] *= 0.5
+    S = Li.T @ P @ Li
+    return 0.5 * (S + S.T)
+
+
+def vgp_training_loss_grads(kind, Z, X, y, Xb, yb, amp, ls, noise, kl_weight, jitter=1e-6,
+                            trace_adjoint=False):
+    """(loss, d/damp, d/dls, d/dnoise, d/dZ) of vgp_training_loss for one kernel (B = 1)."""
+    Z = np.asarray(Z, dtype=np.float64).reshape(len(Z), -1)
+    X = np.asarray(X, dtype=np.float64).reshape(len(X), -1)
+    Xb = np.asarray(Xb, dtype=np.float64).reshape(len(Xb), -1)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    yb = np.asarray(yb, dtype=np.float64).reshape(-1)
+    a, l, s, j, w = float(amp), float(ls), float(noise), float(jitter), float(kl_weight)
+    M, nb = Z.shape[0], yb.size
+    I = np.eye(M)
+    Kzz = kernel_matrix(kind, Z, Z, a, l)[0]
+    Kzx = kernel_matrix(kind, Z, X, a, l)[0]
+    Kzb = kernel_matrix(kind, Z, Xb, a, l)[0]
+    # optimal posterior
+    P0 = Kzx @ Kzx.T
+    Sinv = Kzz + P0 / s + j * I
+    Li = np.linalg.inv(np.linalg.cholesky(Sinv))
+    c = Kzx @ y
+    t = Li.T @ (Li @ c)
+    m = Kzz @ t / s
+    A = Li @ Kzz
+    # variational loss
+    Lzi = np.linalg.inv(np.linalg.cholesky(Kzz + j * I))
+    Kzj_inv = Lzi.T @ Lzi
+    v = Kzj_inv @ m
+    r = yb - Kzb.T @ v
+    s2 = s + j
+    obs = -0.5 * r @ r / s2 - 0.5 * nb * np.log(2 * np.pi * s2)
+    G = Lzi @ Kzb
+    H = Lzi.T @ G
+    R = (A.T if trace_adjoint else A) @ H
+    T = 0.5 * (nb * a * a - np.sum(G * G) + np.sum(R * R)) / s
+    Lpi = np.linalg.inv(np.linalg.cholesky(Kzz + (s + 1e-6) * I))
+    Kp_inv = Lpi.T @ Lpi
+    Lk = np.linalg.cholesky(Kzz)
+    logdetA = 2 * np.sum(np.log(np.diag(Lk))) + np.sum(np.log(np.diag(Li)))
+    KL = (np.sum(np.log(np.diag(np.linalg.inv(Lpi)))) - logdetA
+          + 0.5 * (-M + np.sum((Lpi @ A) ** 2) + np.sum((Lpi @ m) ** 2)))
+    E = obs - T - w * KL
+    # ---- reverse pass for E ----
+    Kzz_b = np.zeros((M, M))
+    Kzb_b = np.zeros_like(Kzb)
+    a_b = 0.0
+    # obs
+    mu_b = r / s2
+    s_b = 0.5 * (r @ r) / s2 ** 2 - 0.5 * nb / s2
+    Kzb_b += np.outer(v, mu_b)
+    u = Kzj_inv @ (Kzb @ mu_b)
+    m_b = u.copy()
+    Kzz_b -= np.outer(u, v)
+    # trace term
+    s_b += T / s
+    a_b += -nb * a / s
+    Kzb_b += H / s
+    Kzz_b -= H @ H.T / (2 * s)
+    if trace_adjoint:
+        A_b = -H @ R.T / s
+        H_b = -A @ R / s
+    else:
+        A_b = -R @ H.T / s
+        H_b = -A.T @ R / s
+    Kzb_b += Kzj_inv @ H_b
+    Kzz_b -= Kzj_inv @ H_b @ H.T
+    # KL
+    A_b += -w * Kp_inv @ A
+    m_b += -w * Kp_inv @ m
+    Kp_b = -0.5 * w * (Kp_inv - Kp_inv @ (A @ A.T + np.outer(m, m)) @ Kp_inv)
+    Kzz_b += Kp_b
+    s_b += np.trace(Kp_b)
+    Lki = np.linalg.inv(Lk)
+    Kzz_b += w * Lki.T @ Lki
+    Sinv_b = -0.5 * w * Li.T @ Li
+    # optimal posterior
+    Kzz_b += np.outer(m_b, t) / s
+    t_b = Kzz @ m_b / s
+    s_b += -(m_b @ m) / s
+    c_b = Li.T @ (Li @ t_b)
+    Sinv_b -= 0.5 * (np.outer(c_b, t) + np.outer(t, c_b))
+    Kzz_b += Li.T @ A_b
+    Sinv_b += _chol_backward(Li, -Li.T @ A_b @ A.T)
+    Kzz_b += Sinv_b
+    Kzx_b = np.outer(c_b, y) + 2.0 * Sinv_b @ Kzx / s
+    s_b += -np.sum(Sinv_b * P0) / s ** 2
+    # kernel VJPs
+    ga1, gl1, Zb1 = kernel_vjp(kind, Z, Z, a, l, Kzz_b + Kzz_b.T)
+    ga2, gl2, Zb2 = kernel_vjp(kind, Z, X, a, l, Kzx_b)
+    ga3, gl3, Zb3 = kernel_vjp(kind, Z, Xb, a, l, Kzb_b)
+    a_b += 0.5 * ga1 + ga2 + ga3
+    l_b = 0.5 * gl1 + gl2 + gl3
+    Z_b = Zb1 + Zb2 + Zb3
+    return -E, -a_b, -l_b, -s_b, -Z_b

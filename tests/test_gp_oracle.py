@@ -72,3 +72,36 @@ def test_vgp_oracle_shapes_and_tightness():
     np.testing.assert_allclose(m_vgp[0], m_exact[0], rtol=1e-4, atol=1e-6)
     L = ogp.vgp_variational_loss("eq", X, X[:10], y[:10], loc, scale, 1.0, 0.5, 0.1, 10 / 30)
     assert np.isfinite(L)
+
+
+@pytest.mark.parametrize("kind", ogp.KERNELS)
+@pytest.mark.parametrize("adjoint", [False, True])
+def test_vgp_training_grads_match_finite_differences(kind, adjoint):
+    """The analytic reverse pass of the VGP training objective (the derivation the HIP path
+    implements) against central differences of the restated loss."""
+    rng = np.random.default_rng(7)
+    N, M, nb = 50, 6, 8
+    X = rng.uniform(-2, 2, (N, 2))
+    y = np.sin(X).sum(1) + 0.1 * rng.normal(size=N)
+    Z = rng.uniform(-2, 2, (M, 2))
+    idx = rng.integers(0, N, nb)
+    a, l, s, w = 0.9, 0.8, 0.3, nb / N
+    L, ga, gl, gs, gZ = ogp.vgp_training_loss_grads(kind, Z, X, y, X[idx], y[idx], a, l, s, w,
+                                                    trace_adjoint=adjoint)
+
+    def f(a_, l_, s_, Z_):
+        return ogp.vgp_training_loss(kind, Z_, X, y, X[idx], y[idx], a_, l_, s_, w,
+                                     trace_adjoint=adjoint)
+    assert L == pytest.approx(f(a, l, s, Z), rel=1e-10)
+    h = 1e-6
+    assert ga == pytest.approx((f(a + h, l, s, Z) - f(a - h, l, s, Z)) / (2 * h), rel=1e-5, abs=1e-6)
+    assert gl == pytest.approx((f(a, l + h, s, Z) - f(a, l - h, s, Z)) / (2 * h), rel=1e-5, abs=1e-6)
+    assert gs == pytest.approx((f(a, l, s + h, Z) - f(a, l, s - h, Z)) / (2 * h), rel=1e-5, abs=1e-6)
+    fz = np.zeros_like(Z)
+    for i in range(M):
+        for k in range(2):
+            Zp, Zm = Z.copy(), Z.copy()
+            Zp[i, k] += h
+            Zm[i, k] -= h
+            fz[i, k] = (f(a, l, s, Zp) - f(a, l, s, Zm)) / (2 * h)
+    np.testing.assert_allclose(gZ, fz, rtol=1e-5, atol=1e-6 * np.abs(fz).max())

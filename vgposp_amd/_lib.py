@@ -57,6 +57,14 @@ SIGNATURES = {
                                     _c_void_p]),
     "vgposp_gemm": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p, _i64,
                            _f64, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p]),
+    "vgposp_gemm_splitk_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32]),
+    "vgposp_gemm_splitk": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p,
+                                  _i64, _f64, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p,
+                                  _size, _c_void_p]),
+    "vgposp_kernel_vjp_workspace_bytes": (_size, [_i64, _i64, _i32]),
+    "vgposp_kernel_vjp": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p,
+                                 _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p,
+                                 _c_void_p, _c_void_p, _size, _c_void_p]),
     "vgposp_potrf_workspace_bytes": (_size, [_i64]),
     "vgposp_potrf_lower": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p,
                                   _c_void_p, _size, _c_void_p]),

@@ -10,6 +10,8 @@
 //   KC image [row][k] with a row pitch of 18 doubles   (operand stored k-contiguous)
 //   MC image [k][row] with a row pitch of 144 doubles  (operand stored row-contiguous)
 // so no operand ever needs an explicit transpose in HBM.
+#include <algorithm>
+
 #include "common.h"
 
 namespace vgposp {
@@ -34,6 +36,11 @@ struct GemmParams {
   double* C;
   int64_t ldc;
   int uplo_c, tri_a, tri_b;
+  // split-K: nsplit > 1 launches nblk * nsplit workgroups; split z covers K range
+  // [z * kchunk, (z + 1) * kchunk) and writes alpha * partial to part + z * m * n (ld n)
+  int nsplit, nblk;
+  int64_t kchunk;
+  double* part;
 };
 
 // Stage one operand tile (128 rows of the M/N dimension x 16 of K) into registers.
@@ -276,6 +283,11 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
     const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
     wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
   }
+  int zsplit = 0;
+  if (p.nsplit > 1) {
+    zsplit = wg / p.nblk;
+    wg -= zsplit * p.nblk;
+  }
   int ti, tj;
   if (p.uplo_c == VGPOSP_LOWER) {
     ti = tri_root(wg);
@@ -306,6 +318,10 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
   if (TRIB) {
     if (TB) kend = min(kend, n0 + GBN);  // stored B[j][k], zero for k > j
     else kbeg = max(kbeg, n0);           // stored B[k][j], zero for j > k
+  }
+  if (p.nsplit > 1) {
+    kbeg = max(kbeg, (int64_t)zsplit * p.kchunk);
+    kend = min(kend, (int64_t)(zsplit + 1) * p.kchunk);
   }
   kbeg = (kbeg / GBK) * GBK;
   if (kend < kbeg) kend = kbeg;
@@ -390,6 +406,10 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
       for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + wm * 64 + i * 16 + fk + 4 * r;
         if (row < p.m && col < p.n && (!lower || col <= row)) {
+          if (p.nsplit > 1) {
+            p.part[(int64_t)zsplit * p.m * p.n + row * p.n + col] = p.alpha * acc[i][j][r];
+            continue;
+          }
           double* c = p.C + row * p.ldc + col;
           double v = p.alpha * acc[i][j][r];
           if (p.beta != 0.0) v += p.beta * *c;
@@ -398,6 +418,22 @@ __global__ __launch_bounds__(256, 1) void gemm_glds_kernel(GemmParams p, int til
       }
     }
   }
+}
+
+// C = sum_z part[z] + beta * C over the (lower) output, fixed summation order.
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int64_t m, int64_t n, int nsplit,
+                                                                 const double* part, double beta,
+                                                                 double* C, int64_t ldc,
+                                                                 int lower) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= m * n) return;
+  const int64_t row = e / n, col = e - row * n;
+  if (lower && col > row) return;
+  double v = 0.0;
+  for (int z = 0; z < nsplit; ++z) v += part[(int64_t)z * m * n + e];
+  double* c = C + row * ldc + col;
+  if (beta != 0.0) v += beta * *c;
+  *c = v;
 }
 
 // y = alpha * A x + beta * y for a single output column (C = A B with n == 1): one wave per row,
@@ -431,9 +467,10 @@ static bool aligned16(const void* ptr, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(ptr) % 16 == 0) && (ld % 2 == 0);
 }
 
-int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
-                const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
-                double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, hipStream_t stream) {
+int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                      const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                      double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
+                      double* part, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
   if (n == 1 && !transa && !tri_a && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
     ProfScope ps("gemv_f64", stream, 2.0 * (double)m * k, 8.0 * ((double)m * k + k + 2.0 * m));
@@ -442,7 +479,7 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
     VG_LAUNCH_CHECK();
     return 0;
   }
-  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b};
+  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr};
   const int va = aligned16(A, lda), vb = aligned16(B, ldb);
   const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
   const bool tri_ok = (!tri_a && !tri_b) || (!transa && !transb && (tri_a != tri_b)) ||
@@ -453,9 +490,15 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
     const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
     // algorithmic flops: a triangular operand halves the useful products
     const double fl = 2.0 * (double)k * outs * ((tri_a && tri_b) ? (1.0 / 3.0) : (tri_a || tri_b) ? 0.5 : 1.0);
+    if (nsplit > 1 && part != nullptr) {
+      p.nblk = (int)nblk;
+      p.kchunk = ceil_div(ceil_div(k, nsplit), GBK) * GBK;
+      p.nsplit = (int)ceil_div(k, p.kchunk);
+      p.part = part;
+    }
     ProfScope ps("gemm_f64", stream, fl,
                  8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
-    dim3 g1((unsigned)nblk);
+    dim3 g1((unsigned)(nblk * p.nsplit));
     if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true>), g1, dim3(256), 0, stream, p, tm, tn);
     else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
     else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false>), g1, dim3(256), 0, stream, p, tm, tn);
@@ -465,6 +508,11 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
     else if (transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<true, false, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
     else hipLaunchKernelGGL((gemm_glds_kernel<true, true, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
     VG_LAUNCH_CHECK();
+    if (p.nsplit > 1) {
+      hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(m * n, 256)), dim3(256),
+                         0, stream, m, n, p.nsplit, part, beta, C, ldc, uplo_c == VGPOSP_LOWER);
+      VG_LAUNCH_CHECK();
+    }
     return 0;
   }
   dim3 grid((unsigned)ceil_div(n, GBN), (unsigned)ceil_div(m, GBM));
@@ -479,7 +527,62 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
   return 0;
 }
 
+int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, hipStream_t stream) {
+  return gemm_launch_split(transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, uplo_c,
+                           tri_a, tri_b, 1, nullptr, stream);
+}
+
+// Split count for a launch with few output tiles and a long K: enough workgroups for 256 CUs
+// (about two per CU), each split at least 512 deep.
+static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c) {
+  const int64_t tm = ceil_div(m, GBM), tn = ceil_div(n, GBN);
+  const int64_t nblk = uplo_c == VGPOSP_LOWER ? tm * (tm + 1) / 2 : tm * tn;
+  int64_t s = ceil_div(512, nblk);
+  s = std::min<int64_t>(s, k / 512);
+  return (int)std::max<int64_t>(s, 1);
+}
+
 }  // namespace vgposp
+
+extern "C" size_t vgposp_gemm_splitk_workspace_bytes(int64_t m, int64_t n, int64_t k, int uplo_c,
+                                                     int splits) {
+  using namespace vgposp;
+  if (m <= 0 || n <= 0 || k <= 0) return 0;
+  if (splits <= 0) splits = auto_splits(m, n, k, uplo_c);
+  return splits > 1 ? 8 * (size_t)splits * m * n : 0;
+}
+
+extern "C" int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, int64_t k,
+                                  double alpha, const double* A, int64_t lda, const double* B,
+                                  int64_t ldb, double beta, double* C, int64_t ldc, int uplo_c,
+                                  int tri_a, int tri_b, int splits, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(m >= 0, 3);
+  VG_CHECK_ARG(n >= 0, 4);
+  VG_CHECK_ARG(k >= 0, 5);
+  VG_CHECK_ARG(A != nullptr || m == 0 || k == 0, 7);
+  VG_CHECK_ARG(lda >= (transa ? (m > 0 ? m : 1) : (k > 0 ? k : 1)), 8);
+  VG_CHECK_ARG(B != nullptr || n == 0 || k == 0, 9);
+  VG_CHECK_ARG(ldb >= (transb ? (k > 0 ? k : 1) : (n > 0 ? n : 1)), 10);
+  VG_CHECK_ARG(C != nullptr || m == 0 || n == 0, 12);
+  VG_CHECK_ARG(ldc >= (n > 0 ? n : 1), 13);
+  VG_CHECK_ARG(uplo_c == VGPOSP_FULL || (uplo_c == VGPOSP_LOWER && m == n), 14);
+  if (m == 0 || n == 0) return 0;
+  if (splits <= 0) splits = k > 0 ? auto_splits(m, n, k, uplo_c) : 1;
+  if (splits > 1) {
+    const size_t need = 8 * (size_t)splits * m * n;
+    if (ws == nullptr || ws_bytes < need) {
+      set_error("vgposp_gemm_splitk: workspace %zu < %zu bytes", ws_bytes, need);
+      return VGPOSP_E_WS;
+    }
+  }
+  return gemm_launch_split(transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, uplo_c,
+                           tri_a, tri_b, splits, static_cast<double*>(ws), as_stream(stream));
+}
 
 extern "C" int vgposp_gemm(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
                            const double* A, int64_t lda, const double* B, int64_t ldb,

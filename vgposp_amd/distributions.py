@@ -23,7 +23,7 @@ import torch
 
 from . import linalg
 from .psd_kernels import _pts
-from .variables import Softplus, Variable, resolve
+from .variables import Placeholder, Softplus, Variable, fed, resolve
 
 LOG_2PI = math.log(2.0 * math.pi)
 
@@ -279,8 +279,14 @@ class VariationalGaussianProcess(GaussianProcess):
 
     def _loc_scale(self):
         B = self._B()
-        loc = linalg.as_device(self.variational_loc)
-        scale = linalg.as_device(self.variational_scale)
+        loc, scale = self.variational_loc, self.variational_scale
+        spec = getattr(loc, "_vgposp_posterior", None)
+        if spec is not None and getattr(scale, "_vgposp_posterior", None) is spec:
+            # the reference's loc / scale are graph tensors of optimal_variational_posterior:
+            # re-evaluate them with the current parameter values, as every sess.run does
+            loc, scale = VariationalGaussianProcess.optimal_variational_posterior(**spec)
+        loc = linalg.as_device(loc)
+        scale = linalg.as_device(scale)
         M = scale.shape[-1]
         loc = loc.reshape(-1, M).expand(B, M).contiguous() if loc.numel() in (M, B * M) else loc
         scale = scale.reshape(-1, M, M).expand(B, M, M).contiguous()
@@ -333,12 +339,25 @@ class VariationalGaussianProcess(GaussianProcess):
         if mean_fn is not None:
             loc = loc + linalg.as_device(mean_fn(Z)).reshape(1, -1)
         if kernel.batch_shape == ():
-            return loc[0], scale[0]
+            loc, scale = loc[0], scale[0]
+        # remember how these were made, so a VGP built on them re-evaluates them when the kernel
+        # parameters / inducing points change (and VGPTrainOp can differentiate through them)
+        spec = dict(kernel=kernel, inducing_index_points=inducing_index_points,
+                    observation_index_points=observation_index_points, observations=observations,
+                    observation_noise_variance=observation_noise_variance, mean_fn=mean_fn,
+                    jitter=jitter)
+        loc._vgposp_posterior = spec
+        scale._vgposp_posterior = spec
         return loc, scale
 
     def variational_loss(self, observations, observation_index_points=None, kl_weight=1.0,
                          name="variational_loss"):
-        """Negative ELBO averaged over the kernel batch (TFP ~0.7 variational_loss)."""
+        """Negative ELBO averaged over the kernel batch (TFP ~0.7 variational_loss).  Returns a
+        ``VariationalLoss``: evaluated now when its inputs are concrete, re-evaluable through
+        ``Session.run`` (placeholders fed), and trainable with ``AdamOptimizer.minimize``."""
+        return VariationalLoss(self, observations, observation_index_points, kl_weight)
+
+    def _variational_loss_value(self, observations, observation_index_points=None, kl_weight=1.0):
         Xb = self.index_points if observation_index_points is None else observation_index_points
         Z = self._Z()
         B = self._B()
@@ -427,5 +446,45 @@ class VariationalGaussianProcess(GaussianProcess):
         return _mvn_sample(mean, L, sample_shape, seed, self.batch_shape != ())
 
 
+class VariationalLoss:
+    """Array-like scalar -ELBO of a VGP (the eager counterpart of the TF1 loss tensor)."""
+
+    def __init__(self, vgp, observations, observation_index_points, kl_weight):
+        self.vgp = vgp
+        self.observations = observations
+        self.observation_index_points = observation_index_points
+        self.kl_weight = float(kl_weight)
+        concrete = not any(isinstance(x, Placeholder)
+                           for x in (observations, observation_index_points))
+        self.value = self.evaluate() if concrete else None
+
+    def inputs(self, feed=None):
+        return fed(self.observations, feed), fed(self.observation_index_points, feed)
+
+    def evaluate(self, feed=None):
+        yb, Xb = self.inputs(feed)
+        self.value = self.vgp._variational_loss_value(yb, Xb, self.kl_weight)
+        return self.value
+
+    def numpy(self):
+        if self.value is None:
+            raise ValueError("variational_loss has unfed placeholders: evaluate it with "
+                             "Session.run(loss, feed_dict=...)")
+        return self.value.detach().cpu().numpy()
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.numpy()
+        return a.astype(dtype) if dtype is not None else a
+
+    def __float__(self):
+        return float(self.numpy())
+
+    def item(self):
+        return float(self)
+
+    def __repr__(self):
+        return f"VariationalLoss({self.value!r})"
+
+
 __all__ = ["GaussianProcess", "GaussianProcessRegressionModel", "VariationalGaussianProcess",
-           "LogProb", "Softplus", "Variable"]
+           "LogProb", "VariationalLoss", "Softplus", "Variable"]

@@ -33,10 +33,11 @@ import torch
 
 from . import linalg
 from .data_generation import sinusoid  # noqa: F401  (gp_functions.py:78-95)
-from .distributions import GaussianProcess, GaussianProcessRegressionModel, LogProb
-from .optimizers import AdamOptimizer, GPTrainOp, Saver, negate
+from .distributions import (GaussianProcess, GaussianProcessRegressionModel, LogProb,
+                            VariationalLoss)
+from .optimizers import AdamOptimizer, GPTrainOp, Saver, VGPTrainOp, negate
 from .psd_kernels import MaternOneHalf
-from .variables import TINY, Softplus, Variable
+from .variables import TINY, Placeholder, Softplus, Variable, placeholder  # noqa: F401
 
 TEST_FN_PARAM = 1
 
@@ -50,12 +51,6 @@ def sinusoid_(x, scale=TEST_FN_PARAM):
 # ---------------------------------------------------------------------------------------------
 # Eager session / placeholder shim
 # ---------------------------------------------------------------------------------------------
-class Placeholder:
-    def __init__(self, shape=None, name=None):
-        self.shape = shape
-        self.name = name
-
-
 class AssignOp:
     """The eager form of ``invert_softplus(placeholder, variable)`` (gp_functions.py:106-109)."""
 
@@ -73,11 +68,21 @@ class Session:
     def run(self, fetches, feed_dict=None):
         feed = feed_dict or {}
         if isinstance(fetches, (list, tuple)):
-            # assignments first (TF runs them before reads that depend on them)
+            # assignments first (TF runs them before reads that depend on them); a train op's
+            # loss fetched in the same run is the value the step was computed from (pre-update),
+            # as in a TF graph where the loss tensor feeds both the fetch and the gradients
             for f in fetches:
                 if isinstance(f, AssignOp):
                     self._eval(f, feed)
-            return [self._eval(f, feed, assigned=True) for f in fetches]
+            memo = {}
+            for f in fetches:
+                if isinstance(f, (GPTrainOp, VGPTrainOp)):
+                    memo[id(f)] = self._eval(f, feed)
+                    src = getattr(f, "loss", None)
+                    if src is not None:
+                        memo[id(src)] = memo[id(f)]
+            return [memo[id(f)] if id(f) in memo else self._eval(f, feed, assigned=True)
+                    for f in fetches]
         return self._eval(fetches, feed)
 
     def _eval(self, f, feed, assigned=False):
@@ -90,6 +95,10 @@ class Session:
         if isinstance(f, GPTrainOp):
             obs = _feed_obs(feed)
             return f.run(obs).detach().cpu().numpy()
+        if isinstance(f, VGPTrainOp):
+            return f.run(feed).detach().cpu().numpy()
+        if isinstance(f, VariationalLoss):
+            return f.evaluate(feed).detach().cpu().numpy()
         if isinstance(f, LogProb):
             obs = _feed_obs(feed)
             if obs is None:

@@ -24,7 +24,13 @@ def device():
 
 
 def _p(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    """Device pointer of a tensor for the C-ABI.  Refuses host tensors: every libvgposp buffer
+    argument is a device pointer, and a host address reaching a kernel is a memory fault."""
+    if t is None:
+        return ctypes.c_void_p(0)
+    if t.device.type != "cuda":
+        raise ValueError(f"libvgposp needs device tensors, got one on {t.device}")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def _stream():
@@ -92,8 +98,10 @@ def kernel_matrix(kind, X1, X2=None, amp=1.0, ls=1.0, diag_shift=None, lower=Fal
 
 
 def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=False,
-         tri_a=False, tri_b=False):
-    """C = alpha op(A) op(B) + beta C on fp64 MFMA (2-D operands)."""
+         tri_a=False, tri_b=False, splitk=False):
+    """C = alpha op(A) op(B) + beta C on fp64 MFMA (2-D operands).  ``splitk=True`` lets the
+    library split a long K over extra workgroups when there are few output tiles (deterministic
+    two-pass reduction through a workspace)."""
     A, B = as_device(A), as_device(B)
     m = A.shape[1] if transa else A.shape[0]
     k = A.shape[0] if transa else A.shape[1]
@@ -104,9 +112,17 @@ def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=
     if C is None:
         C = torch.zeros((m, n), dtype=F64, device=A.device)
         beta = 0.0
+    uplo = LOWER if lower_c else FULL
+    if splitk:
+        nbytes = query("vgposp_gemm_splitk_workspace_bytes", m, n, k, uplo, 0)
+        if nbytes:
+            ws = workspace(nbytes)
+            call("vgposp_gemm_splitk", int(transa), int(transb), m, n, k, float(alpha), _p(A),
+                 A.stride(0), _p(B), B.stride(0), float(beta), _p(C), C.stride(0), uplo,
+                 int(tri_a), int(tri_b), 0, _p(ws), ws.numel(), _stream())
+            return C
     call("vgposp_gemm", int(transa), int(transb), m, n, k, float(alpha), _p(A), A.stride(0), _p(B),
-         B.stride(0), float(beta), _p(C), C.stride(0), LOWER if lower_c else FULL, int(tri_a),
-         int(tri_b), _stream())
+         B.stride(0), float(beta), _p(C), C.stride(0), uplo, int(tri_a), int(tri_b), _stream())
     return C
 
 

@@ -18,7 +18,7 @@ import torch
 
 from . import linalg
 from ._lib import call
-from .variables import Softplus, Variable
+from .variables import Softplus, Variable, resolve
 
 
 class AdamOptimizer:
@@ -30,13 +30,18 @@ class AdamOptimizer:
         self.epsilon = float(epsilon)
         self.name = name
 
-    def minimize(self, loss, var_list=None):
-        """``loss``: a ``distributions.LogProb`` to MAXIMISE (the reference passes ``-feature``;
-        see ``negate``) or a ``Negated`` LogProb.  Returns a ``GPTrainOp``."""
+    def minimize(self, loss, var_list=None, group=None):
+        """``loss``: ``-log_prob`` of a GaussianProcess (a ``Negated`` LogProb, see ``negate``;
+        gp_functions.tf_train_gp_adam) -> ``GPTrainOp``, or a VGP ``variational_loss``
+        (variational_Gaussian_process_example.py:95-102) -> ``VGPTrainOp``.  ``group``: a
+        torch.distributed group over which the VGP's observations are sharded."""
+        from .distributions import VariationalLoss
         if isinstance(loss, Negated):
             return GPTrainOp(loss.log_prob, self, var_list)
-        raise TypeError("minimize() expects -log_prob (a Negated LogProb); "
-                        "use gp_functions.tf_train_gp_adam(log_likelihood, lr)")
+        if isinstance(loss, VariationalLoss):
+            return VGPTrainOp(loss, self, var_list, group)
+        raise TypeError("minimize() expects -log_prob (a Negated LogProb) or a VGP "
+                        "variational_loss")
 
 
 class Negated:
@@ -53,6 +58,7 @@ class GPTrainOp:
     pre-update LML [B] (device tensor), as sess.run([train_op, log_likelihood]) does."""
 
     def __init__(self, log_prob, opt, var_list=None):
+        self.loss = log_prob
         self.gp = log_prob.dist
         self.observations = log_prob.observations
         self.opt = opt
@@ -99,6 +105,90 @@ class GPTrainOp:
 
     def variables(self):
         return {name: sp for name, (_, _, sp) in self.slices.items()}
+
+
+def _adam(theta, grad, m, v, step_count, opt, grad_scale):
+    call("vgposp_adam_update", ctypes.c_void_p(theta.data_ptr()), ctypes.c_void_p(grad.data_ptr()),
+         ctypes.c_void_p(m.data_ptr()), ctypes.c_void_p(v.data_ptr()), theta.numel(), opt.lr,
+         opt.beta1, opt.beta2, opt.epsilon, ctypes.c_void_p(step_count.data_ptr()), grad_scale,
+         linalg._stream())
+
+
+class VGPTrainOp:
+    """One TF1-Adam step on a VGP's variational_loss whose q(u) is optimal_variational_posterior
+    (the reference's training graph, variational_Gaussian_process_example.py:51-102).  Trainables:
+    the kernel's softplus amplitude / length_scale, the softplus observation noise variance and
+    the inducing_index_points Variable, re-bound into one flat device buffer updated by the HIP
+    Adam kernel.  ``run(feed)`` returns the pre-update loss (device scalar)."""
+
+    def __init__(self, loss, opt, var_list=None, group=None):
+        from .vgp_training import VGPObjective
+        vgp = loss.vgp
+        spec = getattr(vgp.variational_loc, "_vgposp_posterior", None)
+        if spec is None:
+            raise NotImplementedError(
+                "VGP training is supported for q(u) = optimal_variational_posterior (the "
+                "reference's graph); free variational loc / scale variables are not")
+        kernel = vgp.kernel
+        if spec["kernel"] is not kernel or kernel.batch_size != 1:
+            raise NotImplementedError("VGP training needs one (non-batched) kernel shared by the "
+                                      "posterior and the VGP")
+        if spec["mean_fn"] is not None or vgp.mean_fn is not None:
+            raise NotImplementedError("VGP training supports the zero mean function only")
+        Z = vgp.inducing_index_points
+        if spec["inducing_index_points"] is not Z:
+            raise ValueError("the posterior and the VGP must share inducing_index_points")
+        self.loss, self.vgp, self.opt = loss, vgp, opt
+        self.params = {"amp": kernel.amplitude, "ls": kernel.length_scale,
+                       "noise": vgp.observation_noise_variance}
+        if spec["observation_noise_variance"] is not self.params["noise"]:
+            raise ValueError("the posterior and the VGP must share observation_noise_variance")
+
+        def chosen(var):
+            return var.trainable and (var_list is None or var in var_list)
+        self.trainable = [(k, p) for k, p in self.params.items()
+                          if isinstance(p, Softplus) and chosen(p.var)]
+        self.train_Z = isinstance(Z, Variable) and chosen(Z)
+        self.Z = Z
+        n = len(self.trainable) + (Z.value.numel() if self.train_Z else 0)
+        dev = linalg.device()
+        self.theta = torch.zeros(max(n, 1), dtype=torch.float64, device=dev)
+        self.grad = torch.zeros_like(self.theta)
+        self.m = torch.zeros_like(self.theta)
+        self.v = torch.zeros_like(self.theta)
+        self.step_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.slot = {}
+        for i, (k, p) in enumerate(self.trainable):
+            p.var._rebind(self.theta[i:i + 1])
+            self.slot[k] = i
+        self.z_off = len(self.trainable)
+        if self.train_Z:
+            Z._rebind(self.theta[self.z_off:])
+        self.objective = VGPObjective(kernel.kind, spec["observation_index_points"],
+                                      spec["observations"], jitter=vgp.jitter,
+                                      posterior_jitter=spec["jitter"],
+                                      trace_adjoint=vgp.trace_adjoint, group=group)
+
+    def _value(self, p):
+        return resolve(p).reshape(())
+
+    def run(self, feed=None):
+        yb, Xb = self.loss.inputs(feed)
+        if Xb is None:
+            Xb = self.vgp.index_points
+        Zv = self.Z.value if isinstance(self.Z, Variable) else linalg.as_device(self.Z)
+        loss, ga, gl, gn, gZ = self.objective.loss_and_grads(
+            Zv, self._value(self.params["amp"]), self._value(self.params["ls"]),
+            self._value(self.params["noise"]), Xb, yb, self.loss.kl_weight)
+        for k, g in (("amp", ga), ("ls", gl), ("noise", gn)):
+            if k in self.slot:
+                i = self.slot[k]
+                self.grad[i:i + 1] = g * self.params[k].dvalue_dvar().reshape(-1)
+        if self.train_Z:
+            self.grad[self.z_off:] = gZ.reshape(-1)
+        _adam(self.theta, self.grad, self.m, self.v, self.step_count, self.opt, 1.0)
+        self.loss.value = loss
+        return loss
 
 
 class Saver:

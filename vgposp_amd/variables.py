@@ -78,6 +78,32 @@ class Softplus:
         return f"Softplus({self.numpy()!r})"
 
 
+class Placeholder:
+    """``tf.placeholder`` stand-in: a named slot filled from ``Session.run(..., feed_dict)``."""
+
+    def __init__(self, shape=None, name=None, dtype=np.float64):
+        self.shape = shape
+        self.name = name
+        self.dtype = dtype
+
+    def __repr__(self):
+        return f"Placeholder({self.name!r}, shape={self.shape})"
+
+
+def placeholder(dtype=np.float64, shape=None, name=None):
+    """tf.placeholder(DTYPE, shape, name) (variational_Gaussian_process_example.py:89-90)."""
+    return Placeholder(shape, name, dtype)
+
+
+def fed(x, feed):
+    """Value of ``x``: looked up in ``feed`` when it is a Placeholder."""
+    if isinstance(x, Placeholder):
+        if feed is None or x not in feed:
+            raise KeyError(f"feed_dict lacks a value for {x!r}")
+        return feed[x]
+    return x
+
+
 def resolve(x, B=None):
     """Current value of a parameter-like as a 1-D float64 device tensor (optionally broadcast)."""
     if x is None:
