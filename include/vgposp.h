@@ -187,6 +187,20 @@ int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int kmax, doubl
                           size_t ws_bytes, void* stream);
 int vgposp_greedy_cache(void* ws, int64_t n, int kmax, double** cache);
 
+/* Placement algorithm 3, the local-kernel greedy (snippets_a3.sparse_placement_algorithm_3,
+ * snippets_a3.py:43-330; with vgposp_greedy_init_ex(..., 1e-6, 1e-7, 1e8, ...) as its tf_nominator
+ * constants).  Per round, after vgposp_greedy_update(round): round 0 scores every candidate into
+ * the cache; round r >= 1 refreshes the cache only for candidates in the index window
+ * [i_d - cutoff, i_d + cutoff) (per grid axis d, clipped, upper bound exclusive) around the
+ * previous pick y* = selected[r-1] of the I0 x I1 x I2 C-order grid (candidates in A -> 0,
+ * cache[y*] = 0); entries outside the window keep their stale values.  Then selects the arg-max of
+ * the cache over the unselected candidates (lowest index on ties).  sel_delta[r] = cache[y];
+ * evals[r] = entries scored this round. */
+int vgposp_greedy_select_window(int64_t n, int kmax, int round, int64_t I0, int64_t I1, int64_t I2,
+                                int cutoff, int64_t c0, int64_t c1, int64_t* selected,
+                                double* sel_delta, int64_t* evals, void* ws, size_t ws_bytes,
+                                void* stream);
+
 /* The two phases of vgposp_greedy_step, for candidate-sharded multi-GPU placement:
  * every rank holds the factored Sigma (replicated init) and owns the candidate slab [c0, c1).
  *   vgposp_greedy_update: rank-1 updates of nom / P_yy and fresh deltas for y in [c0, c1) only
@@ -229,6 +243,9 @@ int vgposp_adam_update(double* theta, const double* grad, double* m, double* v, 
 int vgposp_prof_enable(int on);
 int vgposp_prof_query(const char* name, double* total_ms, int64_t* launches, double* flops,
                       double* bytes);
+/* Text summary of all records: one "name<TAB>ms<TAB>launches<TAB>flops<TAB>bytes" line per
+ * distinct kernel name.  Returns the size needed (with the NUL); buf may be NULL. */
+int64_t vgposp_prof_dump(char* buf, size_t len);
 
 #ifdef __cplusplus
 }

@@ -295,3 +295,79 @@ def sparse_placement_algorithm_2(cov_vv, k, COVER_spatial, trace=None, jitter=TF
         dci[:, r] = cache                                          # :778
         cache[y] = 0.0                                             # :796
     return sorted(A), len(A), dci, sel
+
+
+# ---------------------------------------------------------------------------------------------
+# Placement algorithm 3, the local-kernel greedy: snippets_a3.sparse_placement_algorithm_3
+# (snippets_a3.py:43-330).  TensorFlow is absent: restated from the source (parity unpinned by
+# execution).  Deltas are the TF variant's (tf_nominator / tf_denominator, jitter 1e-6,
+# threshold 1e-7, INF 1e8); after each pick only the index window around it is re-scored.
+# ---------------------------------------------------------------------------------------------
+def _window(y, cover, cutoff):
+    I0, I1, I2 = (int(c) for c in cover[:3])
+    i0, r = divmod(int(y), I1 * I2)
+    i1, i2 = divmod(r, I2)
+    for j0 in range(max(i0 - cutoff, 0), min(i0 + cutoff, I0)):      # :300-305 (upper exclusive)
+        for j1 in range(max(i1 - cutoff, 0), min(i1 + cutoff, I1)):  # :284-289
+            for j2 in range(max(i2 - cutoff, 0), min(i2 + cutoff, I2)):  # :268-273
+                yield j0 * I1 * I2 + j1 * I2 + j2
+
+
+def sparse_placement_algorithm_3(cov_vv, k, COVER_spatial, cutoff, order=None, jitter=TF_JITTER,
+                                 small=TF_SMALL):
+    """snippets_a3.py:43-330 -> (A sorted, final cache [N], delta_cached_iters [N, k]).
+    ``order`` (list) receives the picks in selection order."""
+    cov = np.asarray(cov_vv, dtype=np.float64)
+    N = cov.shape[0]
+    if N != int(np.prod(COVER_spatial[:3])):                        # :51 tf.Assert
+        raise ValueError("N != prod(COVER_spatial)")
+    A, A_bar = [], list(range(N))
+
+    def delta(y):                                                   # body_D :72-112
+        nom = tf_nominator(y, A, cov, jitter)
+        denom = tf_denominator(y, A_bar, cov, jitter)
+        return 0.0 if (abs(denom) < small or abs(nom) < small) else nom / denom
+
+    cache = np.full(N, TF_INF)
+    dci = np.zeros((N, k))
+    for y in range(N):                                              # :116-119 (loop_D)
+        cache[y] = delta(y)
+    dci[:, 0] = cache                                               # :121-124
+    for i in range(k - 1):                                          # body_A :127-322
+        y = sparse_argmax_cache_linear(cache, A, N)
+        A.append(y)
+        A_bar.remove(y)
+        cache[y] = 0.0                                              # :151-156
+        for yj in _window(y, COVER_spatial, cutoff):                # :196-308
+            cache[yj] = 0.0 if yj in A else delta(yj)
+        cache[y] = 0.0                                              # :309-314
+        dci[:, i + 1] = cache                                       # :315-320
+    y = sparse_argmax_cache_linear(cache, A, N)                     # :326-328
+    A.append(y)
+    if order is not None:
+        order.extend(A)
+    return sorted(A), cache, dci
+
+
+def placement_window_precision(cov_vv, k, COVER_spatial, cutoff, jitter=TF_JITTER, thr=TF_SMALL):
+    """Algorithm 3 with the precision-matrix deltas (the HIP path's algebra): (order, cache, dci)."""
+    cov = np.asarray(cov_vv, dtype=np.float64)
+    N = cov.shape[0]
+    A = []
+    delta, _, _ = all_deltas(cov, A, jitter, thr)
+    cache = delta.copy()
+    dci = np.zeros((N, k))
+    dci[:, 0] = cache
+    sel = np.zeros(N, dtype=bool)
+    for i in range(k - 1):
+        y = int(np.flatnonzero(~sel)[np.argmax(cache[~sel])])
+        A.append(y)
+        sel[y] = True
+        delta, _, _ = all_deltas(cov, A, jitter, thr)
+        cache[y] = 0.0
+        for yj in _window(y, COVER_spatial, cutoff):
+            cache[yj] = 0.0 if sel[yj] else delta[yj]
+        dci[:, i + 1] = cache
+    y = int(np.flatnonzero(~sel)[np.argmax(cache[~sel])])
+    A.append(y)
+    return A, cache, dci

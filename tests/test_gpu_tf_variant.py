@@ -77,3 +77,40 @@ def test_tf_constants_equal_alg2_on_goldens():
         _, _, _, sel = sparse_placement_algorithm_2(cov, e["k"], (N, 1, 1), jitter=0.0,
                                                     threshold=1e-8, cache_init=float("inf"))
         assert [int(v) for v in sel[:, 0]] == e["alg2"], name
+
+
+@pytest.mark.parametrize("shape,k,cutoff,nugget", [((4, 4, 4), 6, 1, 1e-2), ((5, 4, 3), 8, 2, 1e-2),
+                                                   ((4, 4, 4), 8, 0, 1e-6)])
+def test_alg3_vs_pinv_oracle(shape, k, cutoff, nugget):
+    from vgposp_amd.snippets_a3 import placement_algorithm_3, sparse_placement_algorithm_3
+    cov = _grid_cov(shape, nugget)
+    order = []
+    rA, rcache, rdci = op.sparse_placement_algorithm_3(cov, k, shape, cutoff, order=order)
+    A, cache, dci = sparse_placement_algorithm_3(cov, k, shape, cutoff)
+    assert list(A.values) == rA
+    assert [int(a) for a in placement_algorithm_3(cov, k, shape, cutoff)] == order
+    fin = rdci < op.TF_INF
+    assert (fin == (dci < op.TF_INF)).all()
+    np.testing.assert_allclose(dci[fin], rdci[fin], rtol=1e-5, atol=1e-8 * np.abs(rdci[fin]).max())
+    np.testing.assert_allclose(cache[:, 0], rcache, rtol=1e-5, atol=1e-8 * np.abs(rdci[fin]).max())
+
+
+@pytest.mark.parametrize("shape,k,cutoff,kind", [((12, 10, 8), 15, 2, "eq"),
+                                                 ((16, 16, 8), 20, 3, "matern52"),
+                                                 ((10, 10, 10), 12, 1, "matern12")])
+def test_alg3_vs_precision_oracle(shape, k, cutoff, kind):
+    from vgposp_amd.snippets_a3 import WindowGreedy
+    cov = _grid_cov(shape, 1e-2, 2.0, kind, seed=5)
+    g = WindowGreedy(cov, k, shape, cutoff, copy=True)
+    g.init()
+    cache = g.cache()
+    snaps = []
+    for _ in range(k):
+        g.step()
+        snaps.append(cache.cpu().numpy().copy())
+    A, deltas, evals = g.result()
+    ref, rcache, rdci = op.placement_window_precision(cov, k, shape, cutoff)
+    assert [int(a) for a in A] == ref
+    np.testing.assert_allclose(np.array(snaps).T, rdci, rtol=1e-7, atol=1e-10 * np.abs(rdci).max())
+    win = min(2 * cutoff, shape[0]) * min(2 * cutoff, shape[1]) * min(2 * cutoff, shape[2])
+    assert evals[0] == cov.shape[0] and all(e <= win for e in evals[1:])

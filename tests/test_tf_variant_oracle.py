@@ -62,3 +62,28 @@ def test_product_cover_assert_before_device_work():
     from vgposp_amd.snippets_a2 import sparse_placement_algorithm_2
     with pytest.raises(ValueError):
         sparse_placement_algorithm_2(np.eye(8), 2, (2, 2, 3))
+
+
+@pytest.mark.parametrize("shape,k,cutoff,nugget", [((4, 4, 4), 6, 1, 1e-2), ((5, 4, 3), 8, 2, 1e-2),
+                                                   ((4, 4, 4), 8, 0, 1e-6)])
+def test_alg3_oracle_forms_agree(shape, k, cutoff, nugget):
+    """snippets_a3 restatement (pinv tf_nominator) vs the precision-matrix form the HIP path
+    implements: same picks, same per-round cache snapshots."""
+    cov = _grid_cov(shape, nugget)
+    order = []
+    A, cache, dci = op.sparse_placement_algorithm_3(cov, k, shape, cutoff, order=order)
+    B, cache2, dci2 = op.placement_window_precision(cov, k, shape, cutoff)
+    assert order == B and A == sorted(B)
+    fin = dci < op.TF_INF
+    assert (fin == (dci2 < op.TF_INF)).all()
+    np.testing.assert_allclose(dci2[fin], dci[fin], rtol=1e-5, atol=1e-8 * np.abs(dci[fin]).max())
+    np.testing.assert_allclose(cache2, dci[:, -1], rtol=1e-5, atol=1e-8 * np.abs(dci[fin]).max())
+
+
+def test_alg3_window_bounds_are_half_open():
+    """The reference's while loops run j in [i - cutoff, min(i + cutoff, I)): 2*cutoff wide."""
+    w = sorted(op._window(0, (4, 4, 4), 2))
+    assert w == sorted(j0 * 16 + j1 * 4 + j2 for j0 in range(2) for j1 in range(2) for j2 in range(2))
+    # cutoff 1 around (1, 1, 1): j in [0, 2) per axis, so the window is lopsided toward 0
+    w = sorted(op._window(1 * 16 + 1 * 4 + 1, (4, 4, 4), 1))
+    assert w == sorted(j0 * 16 + j1 * 4 + j2 for j0 in range(2) for j1 in range(2) for j2 in range(2))

@@ -1,0 +1,100 @@
+"""Time the VGP training step on one GPU, with a per-kernel breakdown.
+
+Workload: N = 64^3 observations on a grid over [-7, 7]^3, M = 8^3 inducing points on the
+sub-grid (spacing 2 = twice the initial length scale, so the unjittered Kzz the KL term factors
+stays well conditioned), EQ kernel with the reference's initial values (softplus(0.54) amp /
+noise, 1e-5 + softplus(0.54) ls), minibatch B, Adam(0.01).  One step = optimal posterior over
+all N + minibatch variational loss + full analytic gradient + Adam update.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from vgposp_amd import _lib
+from vgposp_amd import distributions as tfd
+from vgposp_amd import psd_kernels as tfkern
+from vgposp_amd.optimizers import AdamOptimizer
+from vgposp_amd.variables import Softplus, Variable, placeholder
+
+
+def c3_problem(n=64, m=8, half=7.0, seed=0):
+    g = np.linspace(-half, half, n)
+    X = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
+    rng = np.random.default_rng(seed)
+    y = np.sum(np.exp(-X ** 2 / 20.0) * np.sin(X), axis=1) + rng.normal(0, 0.1, len(X))
+    gz = np.linspace(-half, half, m)
+    Z = np.stack(np.meshgrid(gz, gz, gz, indexing="ij"), -1).reshape(-1, 3)
+    return X, y, Z
+
+
+def build(X, y, Z, B):
+    amp = Softplus(Variable(0.54, name="amplitude"), offset=0.0)
+    ls = Softplus(Variable(0.54, name="length_scale"), offset=1e-5)
+    kernel = tfkern.ExponentiatedQuadratic(amplitude=amp, length_scale=ls)
+    noise = Softplus(Variable(0.54, name="observation_noise_variance"), offset=0.0)
+    Zv = Variable(Z, name="inducing_index_points")
+    loc, scale = tfd.VariationalGaussianProcess.optimal_variational_posterior(
+        kernel=kernel, inducing_index_points=Zv, observation_index_points=X, observations=y,
+        observation_noise_variance=noise)
+    vgp = tfd.VariationalGaussianProcess(kernel, index_points=Z[:8], inducing_index_points=Zv,
+                                         variational_inducing_observations_loc=loc,
+                                         variational_inducing_observations_scale=scale,
+                                         observation_noise_variance=noise)
+    xb = placeholder(np.float64, [B, 3], name="x_train_batch")
+    yb = placeholder(np.float64, [B], name="y_train_batch")
+    loss = vgp.variational_loss(observations=yb, observation_index_points=xb,
+                                kl_weight=float(B) / float(len(X)))
+    return AdamOptimizer(learning_rate=0.01).minimize(loss), loss, xb, yb
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--m", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=32768)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    X, y, Z = c3_problem(args.n, args.m)
+    N, B = len(X), args.batch
+    train_op, loss, xb, yb = build(X, y, Z, B)
+    rng = np.random.default_rng(1)
+    Xd = torch.as_tensor(X, device="cuda")
+    yd = torch.as_tensor(y, device="cuda")
+    batches = [torch.as_tensor(rng.integers(0, N, B), device="cuda")
+               for _ in range(args.warmup + args.steps)]
+    losses = []
+    for i in range(args.warmup):
+        losses.append(float(train_op.run({xb: Xd[batches[i]], yb: yd[batches[i]]})))
+    torch.cuda.synchronize()
+    _lib.prof_enable(True)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        l_ = train_op.run({xb: Xd[batches[i]], yb: yd[batches[i]]})
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    losses.append(float(l_))
+    prof = {}
+    for name in ("kernel_matrix", "gemm_f64", "gemv_f64", "kernel_vjp", "potrf_diag"):
+        ms, launches, flops, nbytes = _lib.prof_query(name)
+        if launches:
+            prof[name] = {"ms_per_step": ms / args.steps, "launches_per_step": launches / args.steps,
+                          "TFLOP/s": flops / (ms * 1e-3) / 1e12 if flops else None,
+                          "GB/s": nbytes / (ms * 1e-3) / 1e9}
+    _lib.prof_enable(False)
+    M = Z.shape[0]
+    print(json.dumps({"N": N, "M": M, "batch": B, "ms_per_step": dt * 1e3,
+                      "elbo_steps_per_s": 1.0 / dt, "loss_first": losses[0], "loss_last": losses[-1],
+                      "flops_2M2N_x2": 4.0 * M * M * N, "breakdown": prof}))
+
+
+if __name__ == "__main__":
+    main()

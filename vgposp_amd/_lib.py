@@ -80,9 +80,13 @@ SIGNATURES = {
     "vgposp_greedy_init_ex": (_i32, [_c_void_p, _i64, _i64, _i32, _f64, _f64, _f64, _c_void_p,
                                      _c_void_p, _size, _c_void_p]),
     "vgposp_greedy_cache": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p)]),
+    "vgposp_greedy_select_window": (_i32, [_i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _i64,
+                                           _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
+                                           _c_void_p]),
     "vgposp_adam_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64, _f64,
                                   _f64, _f64, _c_void_p, _f64, _c_void_p]),
     "vgposp_prof_enable": (_i32, [_i32]),
+    "vgposp_prof_dump": (_i64, [ctypes.c_char_p, _size]),
     "vgposp_prof_query": (_i32, [ctypes.c_char_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64),
                                  ctypes.POINTER(_f64), ctypes.POINTER(_f64)]),
     "vgposp_greedy_update": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i64, _i64, _c_void_p,
@@ -161,3 +165,18 @@ def prof_query(name):
     call("vgposp_prof_query", name.encode(), ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl),
          ctypes.byref(by))
     return ms.value, n.value, fl.value, by.value
+
+
+def prof_dump():
+    """{name: (ms, launches, flops, bytes)} of everything recorded since prof_enable."""
+    fn = load().vgposp_prof_dump
+    need = fn(None, 0)
+    if need < 0:
+        raise VgpospError(last_error())
+    buf = ctypes.create_string_buffer(int(need))
+    fn(buf, need)
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, ms, n, fl, by = line.split("\t")
+        out[name] = (float(ms), int(n), float(fl), float(by))
+    return out

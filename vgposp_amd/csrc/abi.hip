@@ -1,4 +1,5 @@
 // ABI version, the thread-local error channel, and optional per-launch event profiling.
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -91,4 +92,37 @@ extern "C" int vgposp_prof_query(const char* name, double* total_ms, int64_t* la
   if (flops) *flops = fl;
   if (bytes) *bytes = by;
   return 0;
+}
+
+// Per-name summary of everything recorded since prof_enable, one "name\tms\tlaunches\tflops\tbytes"
+// line per distinct name (sorted by name).  Returns the bytes needed (including the final NUL);
+// writes at most `len` bytes into buf (may be NULL to size the buffer).
+extern "C" int64_t vgposp_prof_dump(char* buf, size_t len) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  struct Agg { double ms = 0, fl = 0, by = 0; int64_t n = 0; };
+  std::map<std::string, Agg> agg;
+  for (size_t i = 0; i < g_nrec; ++i) {
+    ProfRec& r = g_recs[i];
+    if (hipEventSynchronize(r.stop) != hipSuccess) return VGPOSP_E_HIP;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, r.start, r.stop) != hipSuccess) return VGPOSP_E_HIP;
+    Agg& a = agg[r.name];
+    a.ms += t;
+    a.fl += r.flops;
+    a.by += r.bytes;
+    ++a.n;
+  }
+  std::string out;
+  char line[512];
+  for (auto& kv : agg) {
+    snprintf(line, sizeof(line), "%s\t%.6f\t%lld\t%.6e\t%.6e\n", kv.first.c_str(), kv.second.ms,
+             (long long)kv.second.n, kv.second.fl, kv.second.by);
+    out += line;
+  }
+  if (buf && len) {
+    size_t n = out.size() < len - 1 ? out.size() : len - 1;
+    memcpy(buf, out.data(), n);
+    buf[n] = '\0';
+  }
+  return (int64_t)out.size() + 1;
 }

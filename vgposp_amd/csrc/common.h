@@ -87,8 +87,8 @@ void prof_end(int slot, hipStream_t s);
 struct ProfScope {
   int slot;
   hipStream_t s;
-  ProfScope(const char* name, hipStream_t st, double flops, double bytes)
-      : slot(prof_on() ? prof_begin(name, st, flops, bytes) : -1), s(st) {}
+  ProfScope(const char* name, hipStream_t st, double flops, double bytes, bool enable = true)
+      : slot(enable && prof_on() ? prof_begin(name, st, flops, bytes) : -1), s(st) {}
   ~ProfScope() {
     if (slot >= 0) prof_end(slot, s);
   }

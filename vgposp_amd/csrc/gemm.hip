@@ -11,6 +11,7 @@
 //   MC image [k][row] with a row pitch of 144 doubles  (operand stored row-contiguous)
 // so no operand ever needs an explicit transpose in HBM.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -498,6 +499,14 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     }
     ProfScope ps("gemm_f64", stream, fl,
                  8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    // optional per-shape breakdown (VGPOSP_PROF_SHAPES=1): "gemm:MxNxK:flags:splits"
+    static const bool shapes = getenv("VGPOSP_PROF_SHAPES") != nullptr;
+    char shape_name[96];
+    if (shapes && prof_on())
+      snprintf(shape_name, sizeof(shape_name), "gemm:%lldx%lldx%lld:%c%c%c%c%c:s%d", (long long)m,
+               (long long)n, (long long)k, transa ? 'T' : 'N', transb ? 'T' : 'N',
+               uplo_c == VGPOSP_LOWER ? 'L' : 'F', tri_a ? 'a' : '-', tri_b ? 'b' : '-', p.nsplit);
+    ProfScope pshape(shape_name, stream, fl, 0.0, shapes && prof_on());
     dim3 g1((unsigned)(nblk * p.nsplit));
     if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true>), g1, dim3(256), 0, stream, p, tm, tn);
     else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true>), g1, dim3(256), 0, stream, p, tm, tn);

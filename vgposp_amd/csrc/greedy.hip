@@ -15,6 +15,7 @@
 // stale entry whose key exceeds the best fresh key is refreshed in bulk (the reference would refresh
 // all of them before it could stop), and the remaining re-score loop runs in one workgroup over
 // per-chunk maxima.  Keys order by value, ties by LOWER index (argmax_cache_linear, :53-67).
+#include <algorithm>
 #include <cfloat>
 
 #include "common.h"
@@ -274,8 +275,64 @@ __global__ __launch_bounds__(CH) void greedy_refresh_kernel(int64_t n, GreedyWS 
   }
 }
 
+// ---- placement algorithm 3 (snippets_a3.py:43-330): the cache is refreshed only inside the
+// index-space window around the last pick; entries outside keep their stale values. ----
+
+// Round 0 (snippets_a3.py:67-119): every candidate is scored once, cache = delta.
+__global__ __launch_bounds__(CH) void greedy_cache_all_kernel(int64_t n, GreedyWS w) {
+  const int64_t i = (int64_t)blockIdx.x * CH + threadIdx.x;
+  if (i < n) w.cache[i] = w.selmask[i] ? 0.0 : w.delta[i];
+  if (i == 0) w.cnt[0] = n;
+}
+
+// Rounds >= 1 (:196-318): for (j0, j1, j2) in [i - cutoff, i + cutoff) clipped to the grid
+// (upper bound exclusive, as the reference's while loops), cache[yj] = delta[yj] or 0 for yj in A;
+// cache[y*] = 0.  cnt[0] = number of window entries (the reference's body_D calls).
+__global__ __launch_bounds__(256) void greedy_window_kernel(const int64_t* selected, int round,
+                                                            int64_t I0, int64_t I1, int64_t I2,
+                                                            int cutoff, GreedyWS w) {
+  const int64_t a = selected[round - 1];
+  const int64_t s0 = I1 * I2;
+  const int64_t i0 = a / s0, i1 = (a - i0 * s0) / I2, i2 = a - i0 * s0 - i1 * I2;
+  const int64_t lo0 = max(i0 - cutoff, (int64_t)0), hi0 = min(i0 + cutoff, I0);
+  const int64_t lo1 = max(i1 - cutoff, (int64_t)0), hi1 = min(i1 + cutoff, I1);
+  const int64_t lo2 = max(i2 - cutoff, (int64_t)0), hi2 = min(i2 + cutoff, I2);
+  const int64_t W0 = max(hi0 - lo0, (int64_t)0), W1 = max(hi1 - lo1, (int64_t)0),
+                W2 = max(hi2 - lo2, (int64_t)0);
+  const int64_t total = W0 * W1 * W2;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j0 = lo0 + t / (W1 * W2), r = t % (W1 * W2);
+    const int64_t j1 = lo1 + r / W2, j2 = lo2 + r % W2;
+    const int64_t yj = j0 * s0 + j1 * I2 + j2;
+    w.cache[yj] = w.selmask[yj] ? 0.0 : w.delta[yj];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.cache[a] = 0.0;
+    w.cnt[0] = total;
+  }
+}
+
+// Per-chunk maxima of the cache over unselected candidates (sparse_argmax_cache_linear, :24-50).
+__global__ __launch_bounds__(CH) void greedy_cache_max_kernel(int64_t n, GreedyWS w) {
+  const int64_t i = (int64_t)blockIdx.x * CH + threadIdx.x;
+  double bv = -DBL_MAX;
+  long long bi = -1;
+  if (i < n && !w.selmask[i]) {
+    bv = w.cache[i];
+    bi = i;
+  }
+  block_keymax(bv, bi);
+  if (threadIdx.x == 0) {
+    w.fval[blockIdx.x] = bv;
+    w.fidx[blockIdx.x] = bi;
+  }
+}
+
 // One workgroup: the remaining re-score loop of placement_algorithm2.py:183-208, then selection.
-__global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round, int lazy,
+// mode: 0 = full greedy (placement_algorithm_1), 1 = lazy (placement_algorithm_2),
+//       2 = window (placement algorithm 3: arg-max of the cache maxima in fval / fidx).
+__global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round, int mode,
                                                            int64_t* selected, double* sel_delta,
                                                            int64_t* evals, GreedyWS w,
                                                            int64_t cbeg, int64_t cend) {
@@ -286,6 +343,7 @@ __global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round,
   double v;
   long long y = -1;
   long long loop_evals = 0;
+  const bool lazy = mode == 1;
   if (!lazy) {
     reduce_keys(w.fval, w.fidx, nch, v, y);
   } else {
@@ -338,8 +396,8 @@ __global__ __launch_bounds__(CH) void greedy_select_kernel(int64_t n, int round,
   const bool own = y >= cbeg && y < cend;
   if (threadIdx.x == 0) {
     selected[round] = y;
-    if (sel_delta) sel_delta[round] = w.delta[y];
-    if (evals) evals[round] = lazy ? w.cnt[0] + loop_evals : n - round;
+    if (sel_delta) sel_delta[round] = mode == 2 ? w.cache[y] : w.delta[y];
+    if (evals) evals[round] = mode != 0 ? w.cnt[0] + loop_evals : n - round;
     w.cnt[0] = 0;
     w.selmask[y] = 1;
     w.piv[0] = own ? w.nom[y] : 0.0;
@@ -473,7 +531,44 @@ extern "C" int vgposp_greedy_select(int64_t n, int kmax, int round, int lazy, in
     VG_LAUNCH_CHECK();
   }
   ProfScope pss("greedy_select", s, 0.0, 0.0);
-  hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(CH), 0, s, n, round, lazy, selected,
+  hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(CH), 0, s, n, round, lazy ? 1 : 0,
+                     selected, sel_delta, evals, w, c0, c1);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_greedy_select_window(int64_t n, int kmax, int round, int64_t I0, int64_t I1,
+                                           int64_t I2, int cutoff, int64_t c0, int64_t c1,
+                                           int64_t* selected, double* sel_delta, int64_t* evals,
+                                           void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  GreedyWS w;
+  double dummy = 0.0;
+  int rc = greedy_check(__func__, &dummy, n, n, kmax, round, ws, ws_bytes, &w);
+  if (rc) return rc;
+  VG_CHECK_ARG(I0 >= 1 && I1 >= 1 && I2 >= 1 && I0 * I1 * I2 == n, 4);
+  VG_CHECK_ARG(cutoff >= 0, 7);
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= n, 8);
+  VG_CHECK_ARG(selected != nullptr, 10);
+  hipStream_t s = as_stream(stream);
+  const unsigned nch = (unsigned)ceil_div(n, CH);
+  {
+    ProfScope psw("greedy_window", s, 0.0, 0.0);
+    if (round == 0) {
+      hipLaunchKernelGGL(greedy_cache_all_kernel, dim3(nch), dim3(CH), 0, s, n, w);
+    } else {
+      const int64_t span = 2 * (int64_t)cutoff;
+      const int64_t total = span * span * span;
+      const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(total, 256), 4096));
+      hipLaunchKernelGGL(greedy_window_kernel, dim3(g), dim3(256), 0, s, selected, round, I0, I1,
+                         I2, cutoff, w);
+    }
+    VG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(greedy_cache_max_kernel, dim3(nch), dim3(CH), 0, s, n, w);
+  VG_LAUNCH_CHECK();
+  ProfScope pss("greedy_select", s, 0.0, 0.0);
+  hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(CH), 0, s, n, round, 2, selected,
                      sel_delta, evals, w, c0, c1);
   VG_LAUNCH_CHECK();
   return 0;
