@@ -9,7 +9,7 @@
 //   trtri_rec(L):  X11 = trtri_rec(L11), X22 = trtri_rec(L22)
 //                  W   = L21 X11               TRMM (X11 lower)        K = n1
 //                  X21 = -X22 W                TRMM (X22 lower)        K = n2
-// Leaves (<= 128) are factored and inverted in LDS by one workgroup (potrf_diag_kernel); their
+// Leaves (<= 128) are factored and inverted in LDS by one workgroup (potrf_leaf_kernel); their
 // inverses are kept in the workspace for the trsm leaves and the trtri leaves.
 //
 // Replaces the Eigen LLT that tf.linalg.cholesky runs inside tfd.GaussianProcess.log_prob
@@ -26,107 +26,211 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
 
 constexpr int NB = 128;        // leaf size (== GEMM tile, so trsm leaves are in place)
 
+
+// ---------------------------------------------------------------------------------------------
+// Blocked leaf: Cholesky + inverse of a jb x jb (jb <= 128) block in LDS, one workgroup of 4 waves.
+// Panels of 16 columns: wave 0 factors the 16x16 diagonal block (and inverts it) with wave-level
+// syncs only; all waves apply it to the rows below (TRSM by the block inverse) and update the
+// trailing lower triangle with v_mfma_f64_16x16x4f64 (16x16 tiles, K = 16).  The inverse is then
+// formed block row by block row:  X_ij = -X_ii * sum_{k=j}^{i-1} L_ik X_kj  (two MFMA chains per
+// 16x16 tile, the first chain's accumulator feeding the second directly as its B operand).
+// ~3 barriers per panel instead of 3 per column.  X (strictly lower) lives transposed in the
+// upper triangle of the LDS image, diag(X) = 1 / diag(L) in rdiag.  jb is padded to a multiple of
+// 16 with an identity block.
+// ---------------------------------------------------------------------------------------------
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// Phase stamps for tools/diag_probe.hip (debug builds only; compiled out otherwise).
 #ifdef VGPOSP_STAMPS
-__device__ long long g_stamps[8];
-#define STAMP(i) \
-  if (threadIdx.x == 0) g_stamps[i] = (long long)__builtin_amdgcn_s_memtime()
+__device__ long long g_stamps[16];
+#define STAMP_NOW() ((long long)__builtin_amdgcn_s_memtime())
+#define STAMP_ADD(i, t0) \
+  if (threadIdx.x == 0) g_stamps[i] += STAMP_NOW() - (t0)
 #else
-#define STAMP(i)
+#define STAMP_NOW() 0LL
+#define STAMP_ADD(i, t0)
 #endif
 
-// Factor and invert the jb x jb diagonal block at A (lower) in LDS, one workgroup:
-//   A_jj lower <- L (invert == 0) or L^-1 (invert == 1),
-//   linv (NB x NB, zero above the diagonal) <- L^-1,
-//   diag_out[c] <- L[c][c],  info <- first failing global column + 1.
-constexpr int DP = NB + 1;  // LDS pitch (conflict-free column walks)
-constexpr int DIAG_THREADS = 1024;
+constexpr int LW = 16;                 // panel width
+constexpr int LP2 = NB + 4;            // LDS pitch (doubles)
+constexpr int LEAF_THREADS = 256;
 
-// Batched use (small matrices): workgroup b handles A + b * stride_a, info + b, diag_out + b * n
-// (linv must then be null).
-__global__ __launch_bounds__(DIAG_THREADS) void potrf_diag_kernel(double* A, int64_t lda, int jb,
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int leaf_tri_root(int t) {
+  int r = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  return r;
+}
+
+// X[R][C] of the inverse (lower, R >= C) from the LDS image.
+__device__ __forceinline__ double xval(const double* L, const double* rdiag, int R, int C) {
+  return R > C ? L[C * LP2 + R] : (R == C ? rdiag[R] : 0.0);
+}
+
+__global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int64_t lda, int jb,
                                                                   int64_t col0, int invert,
                                                                   double* linv, double* diag_out,
-                                                                  int* info, int64_t stride_a = 0) {
-  extern __shared__ double L[];  // [NB][DP]; X (the inverse) lives transposed in the upper part
-  __shared__ double rdiag[NB];   // 1 / L[r][r]
-  const int t = threadIdx.x;
+                                                                  int* info, int64_t stride_a) {
+  extern __shared__ double L[];  // [NB][LP2]
+  __shared__ double rdiag[NB];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   A += blockIdx.x * stride_a;
   info += blockIdx.x;
   if (diag_out) diag_out += (int64_t)blockIdx.x * jb;
-  const int tx = t & 31, ty = t >> 5;
-  for (int e = t; e < jb * jb; e += DIAG_THREADS) {
-    const int r = e / jb, c = e % jb;
-    if (c <= r) L[r * DP + c] = A[(int64_t)r * lda + c];
+  const int JP = (jb + LW - 1) & ~(LW - 1), NP = JP / LW;
+  for (int e = t; e < JP * JP; e += LEAF_THREADS) {
+    const int r = e / JP, c = e - r * JP;
+    if (c <= r) L[r * LP2 + c] = r < jb ? A[(int64_t)r * lda + c] : (r == c ? 1.0 : 0.0);
   }
   __syncthreads();
-  STAMP(0);
+  const int fr = lane & 15, fk = lane >> 4;
+  long long ts = STAMP_NOW();
 
-  // Unblocked right-looking Cholesky; the trailing update walks a 32x32 thread grid (no integer
-  // division), each thread keeping its column multiplier of the step in a register.
-  for (int c = 0; c < jb; ++c) {
-    const double d = L[c * DP + c];
-    const double piv = sqrt(d);
-    const double inv = 1.0 / piv;
-    if (t == 0) {
-      if (!(d > 0.0)) atomicCAS(info, 0, (int)(col0 + c + 1));  // first failure
-      rdiag[c] = inv;
-    }
-    __syncthreads();
-    for (int r = c + 1 + t; r < jb; r += DIAG_THREADS) L[r * DP + c] *= inv;
-    if (t == 0) L[c * DP + c] = piv;
-    __syncthreads();
-    for (int r = c + 1 + ty; r < jb; r += 32) {
-      const double lr = L[r * DP + c];
-      for (int s2 = c + 1 + tx; s2 <= r; s2 += 32) L[r * DP + s2] -= lr * L[s2 * DP + c];
-    }
-    __syncthreads();
-  }
-  STAMP(1);
-
-  // Triangular inverse X = L^-1, column c by a group of 8 lanes:
-  //   X[c][c] = 1/L[c][c];  X[r][c] = -(sum_{k=c}^{r-1} L[r][k] X[k][c]) / L[r][r]
-  // X[r][c] (r > c) is kept at L[c][r] (upper part), X[c][c] at L[c][c] after the copy-out of L
-  // (diag(L) is saved first).  Four independent partial sums keep the LDS reads in flight.
-  {
-    const int c = t >> 3, g = t & 7;
-    if (c < jb) {
-      const double xcc = rdiag[c];
-      for (int r = c + 1; r < jb; ++r) {
-        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-        int k = c + g;
-        for (; k + 24 < r; k += 32) {
-          s0 += L[r * DP + k] * (k == c ? xcc : L[c * DP + k]);
-          s1 += L[r * DP + k + 8] * L[c * DP + k + 8];
-          s2 += L[r * DP + k + 16] * L[c * DP + k + 16];
-          s3 += L[r * DP + k + 24] * L[c * DP + k + 24];
+  for (int p = 0; p < NP; ++p) {
+    const int c0 = p * LW;
+    if (wave == 0) {
+      // unblocked Cholesky of the 16x16 diagonal block
+      for (int c = 0; c < LW; ++c) {
+        const int cc = c0 + c;
+        const double d = L[cc * LP2 + cc];
+        const double piv = sqrt(d), inv = 1.0 / piv;
+        if (lane > c && lane < LW) L[(c0 + lane) * LP2 + cc] *= inv;
+        if (lane == 0) {
+          if (!(d > 0.0) && cc < jb) atomicCAS(info, 0, (int)(col0 + cc + 1));
+          rdiag[cc] = inv;
+          L[cc * LP2 + cc] = piv;
         }
-        for (; k < r; k += 8) s0 += L[r * DP + k] * (k == c ? xcc : L[c * DP + k]);
-        double s = (s0 + s1) + (s2 + s3);
-        s += __shfl_xor(s, 1, 8);
-        s += __shfl_xor(s, 2, 8);
-        s += __shfl_xor(s, 4, 8);
-        if (g == 0) L[c * DP + r] = -s * rdiag[r];
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();
+        for (int e = lane; e < LW * LW; e += 64) {
+          const int r = e >> 4, s2 = e & 15;
+          if (s2 > c && s2 <= r) L[(c0 + r) * LP2 + c0 + s2] -= L[(c0 + r) * LP2 + cc] * L[(c0 + s2) * LP2 + cc];
+        }
+        wave_sync();
+      }
+      STAMP_ADD(0, ts);
+      ts = STAMP_NOW();
+      // its inverse by rows, X[r][j] = -(sum_{k=j}^{r-1} L[r][k] X[k][j]) / L[r][r], stored
+      // transposed in the block's upper part; 4 lanes split each sum
+      {
+        const int j = lane & 15, part = lane >> 4;
+        for (int r = 1; r < LW; ++r) {
+          double acc = 0.0;
+          if (j < r) {
+            for (int k = j + part; k < r; k += 4)
+              acc += L[(c0 + r) * LP2 + c0 + k] * (k == j ? rdiag[c0 + j] : L[(c0 + j) * LP2 + c0 + k]);
+          }
+          acc += __shfl_xor(acc, 16, 64);
+          acc += __shfl_xor(acc, 32, 64);
+          if (part == 0 && j < r) L[(c0 + j) * LP2 + c0 + r] = -acc * rdiag[c0 + r];
+          wave_sync();
+        }
       }
     }
+    __syncthreads();
+    STAMP_ADD(1, ts);
+    ts = STAMP_NOW();
+    // rows below: P[r][j] = sum_{k <= j} L[r][c0+k] X[j][k]; thread (j = t & 15) owns rows
+    // c0 + 16 + (t >> 4) + 16 q, whose sums run as independent chains over k
+    constexpr int NQ = (NB - LW) / 16;
+    {
+      const int j = t & 15, rb = c0 + LW + (t >> 4);
+      double acc[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r = rb + 16 * q;
+        acc[q] = r < JP ? L[r * LP2 + c0 + j] * rdiag[c0 + j] : 0.0;
+      }
+      for (int k = 0; k < j; ++k) {
+        const double xk = L[(c0 + k) * LP2 + c0 + j];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int r = rb + 16 * q;
+          if (r < JP) acc[q] += L[r * LP2 + c0 + k] * xk;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int r = rb + 16 * q;
+        if (r < JP) L[r * LP2 + c0 + j] = acc[q];
+      }
+    }
+    __syncthreads();
+    STAMP_ADD(2, ts);
+    ts = STAMP_NOW();
+    // trailing lower triangle -= P P^T on MFMA, 16x16 tiles
+    const int NT = NP - p - 1, ntile = NT * (NT + 1) / 2;
+    for (int tt = wave; tt < ntile; tt += 4) {
+      const int ti = leaf_tri_root(tt), tj = tt - ti * (ti + 1) / 2;
+      const int r0 = c0 + LW + LW * ti, s0 = c0 + LW + LW * tj;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const double a = L[(r0 + fr) * LP2 + c0 + 4 * s4 + fk];
+        const double b = L[(s0 + fr) * LP2 + c0 + 4 * s4 + fk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int row = r0 + fk + 4 * reg, col = s0 + fr;
+        if (ti != tj || col <= row) L[row * LP2 + col] -= acc[reg];
+      }
+    }
+    __syncthreads();
+    STAMP_ADD(3, ts);
+    ts = STAMP_NOW();
   }
-  __syncthreads();
-  STAMP(2);
 
-  for (int e = t; e < NB * NB; e += DIAG_THREADS) {
-    const int r = e / NB, c = e % NB;
-    double x = 0.0;
-    if (r < jb && c < jb && c <= r) x = (r == c) ? rdiag[c] : L[c * DP + r];
-    if (linv) linv[e] = x;
-    if (r < jb && c <= r) {
-      A[(int64_t)r * lda + c] = invert ? x : L[r * DP + c];
+  if (invert || linv) {
+    for (int i = 1; i < NP; ++i) {
+      const int i0 = i * LW;
+      for (int j = wave; j < i; j += 4) {
+        const int j0 = j * LW;
+        dbl4 S = {0.0, 0.0, 0.0, 0.0};
+        for (int k = j; k < i; ++k) {
+          const int k0 = k * LW;
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const double a = L[(i0 + fr) * LP2 + k0 + 4 * s4 + fk];
+            const double b = xval(L, rdiag, k0 + 4 * s4 + fk, j0 + fr);
+            S = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, S, 0, 0, 0);
+          }
+        }
+        dbl4 X = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const double a = xval(L, rdiag, i0 + fr, i0 + 4 * s4 + fk);
+          X = __builtin_amdgcn_mfma_f64_16x16x4f64(a, S[s4], X, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) L[(j0 + fr) * LP2 + i0 + fk + 4 * reg] = -X[reg];
+      }
+      __syncthreads();
     }
   }
-  if (diag_out != nullptr) {
-    for (int c = t; c < jb; c += DIAG_THREADS) diag_out[c] = L[c * DP + c];
+  STAMP_ADD(4, ts);
+  ts = STAMP_NOW();
+
+  for (int e = t; e < NB * NB; e += LEAF_THREADS) {
+    const int r = e / NB, c = e % NB;
+    double x = 0.0;
+    if (r < jb && c <= r) x = (r == c) ? rdiag[c] : L[c * LP2 + r];
+    if (linv) linv[e] = x;
+    if (r < jb && c <= r) A[(int64_t)r * lda + c] = invert ? x : L[r * LP2 + c];
   }
-  STAMP(3);
+  if (diag_out != nullptr) {
+    for (int c = t; c < jb; c += LEAF_THREADS) diag_out[c] = L[c * LP2 + c];
+  }
+  STAMP_ADD(5, ts);
 }
+
+static size_t leaf_shmem() { return (size_t)NB * LP2 * sizeof(double); }
 
 // A (jb x jb lower) <- linv (the saved leaf inverse)
 __global__ void copy_leaf_kernel(double* A, int64_t lda, int jb, const double* linv) {
@@ -150,13 +254,12 @@ struct Fact {
   double* leaf(int64_t col0) const { return linv_all + (col0 / NB) * NB * NB; }
 };
 
-static size_t diag_shmem() { return (size_t)NB * DP * sizeof(double); }
 
 static int leaf_factor(const Fact& f, double* A, int jb, int64_t col0, int invert) {
   ProfScope ps("potrf_diag", f.s, 2.0 * jb * (double)jb * jb / 3.0, 8.0 * jb * (double)jb * 2);
-  hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(DIAG_THREADS), diag_shmem(), f.s, A, f.lda,
+  hipLaunchKernelGGL(potrf_leaf_kernel, dim3(1), dim3(LEAF_THREADS), leaf_shmem(), f.s, A, f.lda,
                      jb, col0, invert, f.leaf(col0), f.diag_out ? f.diag_out + col0 : nullptr,
-                     f.info);
+                     f.info, (int64_t)0);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -228,8 +331,8 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
               void* ws, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    VG_HIP(hipFuncSetAttribute((const void*)potrf_diag_kernel,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)diag_shmem()));
+    VG_HIP(hipFuncSetAttribute((const void*)potrf_leaf_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf_shmem()));
     attr_set = true;
   }
   const int64_t leaves = (n + NB - 1) / NB;
@@ -269,12 +372,12 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
     // one launch, one workgroup per matrix (e.g. the calc_H likelihood surface)
     static bool attr_set = false;
     if (!attr_set) {
-      VG_HIP(hipFuncSetAttribute((const void*)potrf_diag_kernel,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)diag_shmem()));
+      VG_HIP(hipFuncSetAttribute((const void*)potrf_leaf_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf_shmem()));
       attr_set = true;
     }
     ProfScope ps("potrf_diag", s, batch * 2.0 * n * (double)n * n / 3.0, batch * 16.0 * n * (double)n);
-    hipLaunchKernelGGL(potrf_diag_kernel, dim3(batch), dim3(DIAG_THREADS), diag_shmem(), s, A, lda,
+    hipLaunchKernelGGL(potrf_leaf_kernel, dim3(batch), dim3(LEAF_THREADS), leaf_shmem(), s, A, lda,
                        (int)n, (int64_t)0, invert, (double*)nullptr, diag_out, info, stride);
     VG_LAUNCH_CHECK();
     return 0;

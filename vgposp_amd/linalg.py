@@ -98,7 +98,7 @@ def kernel_matrix(kind, X1, X2=None, amp=1.0, ls=1.0, diag_shift=None, lower=Fal
 
 
 def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=False,
-         tri_a=False, tri_b=False, splitk=False):
+         tri_a=False, tri_b=False, splitk=True):
     """C = alpha op(A) op(B) + beta C on fp64 MFMA (2-D operands).  ``splitk=True`` lets the
     library split a long K over extra workgroups when there are few output tiles (deterministic
     two-pass reduction through a workspace)."""
