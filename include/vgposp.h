@@ -110,6 +110,26 @@ int vgposp_kernel_vjp(int kind, const double* X1, int64_t n1, const double* X2, 
                       size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Covariance builders (cov_vv on device).
+ * vgposp_kernel_matvec: out[i] = sum_j K(X1_i, X2_j) v[j] + beta * out[i] for one kernel (amp, ls:
+ *   device [1]), without materialising K: the VGP / GPRM predictive mean at many points, e.g. the
+ *   tracer value at every (location, T/P sample) 5-D point that main_architecture_2_
+ *   sampledistribution.py:432-458 evaluates one vgp.mean() at a time.
+ * vgposp_center_rows: T[i][0:s] <- (T[i][:] - mean(T[i][:])) * scale.  A SYRK of the result
+ *   (vgposp_gemm, alpha = 1/s) is tfp.stats.covariance(t_i, t_j, sample_axis=0) for every pair
+ *   (main.py:190-199, main_architecture_2_sampledistribution.py:470-479).
+ * vgposp_index_taper: C[i][j] *= g(|idx_i - idx_j|), g(d) = exp(-(beta d)^2 / (2 pi)), 0 where
+ *   g < threshold, over an I0 x I1 x I2 C-order grid (the beta-decay local kernel filter,
+ *   main_architecture_2_sampledistribution.py:361-421; threshold 0.01 there).  uplo as elsewhere.
+ * --------------------------------------------------------------------------------------------- */
+int vgposp_kernel_matvec(int kind, const double* X1, int64_t n1, const double* X2, int64_t n2,
+                         int d, const double* amp, const double* ls, const double* v, double beta,
+                         double* out, void* stream);
+int vgposp_center_rows(double* T, int64_t n, int64_t s, int64_t ld, double scale, void* stream);
+int vgposp_index_taper(double* C, int64_t n, int64_t ldc, int64_t I0, int64_t I1, int64_t I2,
+                       double beta, double threshold, int uplo, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Blocked right-looking Cholesky, lower, in place.  Replaces tf.linalg.cholesky inside
  * tfd.GaussianProcess.log_prob / GPRM / VGP (gp_functions.py:166-172, main.py:105,
  * 3D_sin_wave.py:172) and is the O(N^3) core of the dense greedy placement.

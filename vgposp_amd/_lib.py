@@ -65,6 +65,11 @@ SIGNATURES = {
     "vgposp_kernel_vjp": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p,
                                  _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p,
                                  _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_kernel_matvec": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p,
+                                    _c_void_p, _c_void_p, _f64, _c_void_p, _c_void_p]),
+    "vgposp_center_rows": (_i32, [_c_void_p, _i64, _i64, _i64, _f64, _c_void_p]),
+    "vgposp_index_taper": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _f64, _f64, _i32,
+                                  _c_void_p]),
     "vgposp_potrf_workspace_bytes": (_size, [_i64]),
     "vgposp_potrf_lower": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p,
                                   _c_void_p, _size, _c_void_p]),

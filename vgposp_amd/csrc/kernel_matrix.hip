@@ -9,27 +9,13 @@
 // of the tile are held in registers, X1 rows are wave-uniform (scalar-cached) loads.
 // Formula, as TFP evaluates it:  K = exp(2 log amp + log k(r / ls)).
 #include "common.h"
+#include "psd.h"
 
 namespace vgposp {
 
 constexpr int KM_ROWS = 32;
 constexpr int KM_COLS = 128;
 constexpr int KM_MAXD = 8;
-
-template <int KIND>
-__device__ __forceinline__ double kfun(double d2, double two_log_amp, double inv_ls, double inv_ls2) {
-  if (KIND == VGPOSP_KERNEL_EQ) {
-    return exp(two_log_amp - 0.5 * d2 * inv_ls2);
-  }
-  const double r = sqrt(d2) * inv_ls;
-  if (KIND == VGPOSP_KERNEL_MATERN12) return exp(two_log_amp - r);
-  if (KIND == VGPOSP_KERNEL_MATERN32) {
-    const double s = 1.7320508075688772 * r;
-    return exp(two_log_amp + log1p(s) - s);
-  }
-  const double s = 2.23606797749979 * r;  // MATERN52
-  return exp(two_log_amp + log1p(s + s * s * (1.0 / 3.0)) - s);
-}
 
 template <int KIND, int D>
 __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, int64_t n1,

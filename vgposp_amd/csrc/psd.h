@@ -1,0 +1,24 @@
+// PSD kernel functions shared by kernel assembly, the kernel-matrix-vector product and friends.
+// As TFP evaluates them:  k(r) = exp(2 log amp + log k_unit(r / ls)).
+#pragma once
+
+#include "common.h"
+
+namespace vgposp {
+
+template <int KIND>
+__device__ __forceinline__ double kfun(double d2, double two_log_amp, double inv_ls, double inv_ls2) {
+  if (KIND == VGPOSP_KERNEL_EQ) {
+    return exp(two_log_amp - 0.5 * d2 * inv_ls2);
+  }
+  const double r = sqrt(d2) * inv_ls;
+  if (KIND == VGPOSP_KERNEL_MATERN12) return exp(two_log_amp - r);
+  if (KIND == VGPOSP_KERNEL_MATERN32) {
+    const double s = 1.7320508075688772 * r;
+    return exp(two_log_amp + log1p(s) - s);
+  }
+  const double s = 2.23606797749979 * r;  // MATERN52
+  return exp(two_log_amp + log1p(s + s * s * (1.0 / 3.0)) - s);
+}
+
+}  // namespace vgposp

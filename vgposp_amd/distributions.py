@@ -401,6 +401,16 @@ class VariationalGaussianProcess(GaussianProcess):
             out.append(obs_ll - trace_term - kl_weight * kl)
         return -torch.mean(torch.stack(out))
 
+    def mean_weights(self):
+        """(w = Kzz^-1 (loc - m(Z)) [M] for kernel batch entry 0, zero-mean flag): the predictive
+        mean is K(x*, Z) w (+ m(x*)), which vgposp_kernel_matvec evaluates without forming K."""
+        loc, _ = self._loc_scale()
+        M = loc.shape[-1]
+        Lzinv, _ = self._kzz_factor()
+        d = (loc[0] - self._mean(self._Z())).reshape(M, 1)
+        w = linalg.gemm(Lzinv[0], linalg.gemm(Lzinv[0], d, tri_a=True), transa=True, tri_a=True)
+        return w.reshape(-1), self.mean_fn is None
+
     def _predictive(self, want_cov=True):
         Xs = self.index_points
         Z = self._Z()
