@@ -47,6 +47,10 @@ def parse():
     p.add_argument("--cpu-shape", type=int, nargs=3, default=[8, 8, 8])
     p.add_argument("--cpu-k", type=int, default=2)
     p.add_argument("--no-potrf", action="store_true", help="skip the separate potrf GF/s run")
+    p.add_argument("--no-vgp", action="store_true", help="skip the C3 VGP training line")
+    p.add_argument("--vgp-steps", type=int, default=10)
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r1.json"),
+                   help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
 
 
@@ -114,6 +118,58 @@ def cpu_baseline(args, N):
     }
 
 
+def load_traffic(path, kernel, N, shape, k):
+    """Per-launch HBM bytes of `kernel` measured by a rocprofv3 PMC pass of this same workload
+    (tools/pmc_traffic.py writes the file; (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 per the gfx950
+    correction in MI355X_MICROARCH.md).  None when absent or measured on another workload."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    w = t.get("workload", {})
+    if w.get("N") != N or list(w.get("shape", [])) != list(shape) or w.get("k") != k:
+        return None
+    kern = t.get("kernels", {}).get(kernel)
+    if not kern:
+        return None
+    return {"bytes_per_launch": kern["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+
+
+def vgp_c3(args):
+    """Config C3: VGP training steps/s at N = 64^3, M = 512, minibatch 32,768 —
+    optimal posterior over all N + minibatch ELBO + analytic gradient + Adam, on this GPU."""
+    import torch
+
+    from vgposp_amd import _lib
+    from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
+    X, y, Z = vgp_c3_data()
+    N, M, B = len(X), len(Z), 32768
+    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B)
+    Xd = torch.as_tensor(X, device="cuda")
+    yd = torch.as_tensor(y, device="cuda")
+    rng = np.random.default_rng(1)
+    idx = [torch.as_tensor(rng.integers(0, N, B), device="cuda") for _ in range(args.vgp_steps + 2)]
+    first = float(train_op.run({xb: Xd[idx[0]], yb: yd[idx[0]]}))
+    train_op.run({xb: Xd[idx[1]], yb: yd[idx[1]]})
+    torch.cuda.synchronize()
+    _lib.prof_enable(True)
+    t0 = time.perf_counter()
+    for i in range(2, args.vgp_steps + 2):
+        last = train_op.run({xb: Xd[idx[i]], yb: yd[idx[i]]})
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.vgp_steps
+    ms, n, fl, _ = _lib.prof_query("gemm_f64")
+    _lib.prof_enable(False)
+    return {"metric": "VGP ELBO Adam steps/sec", "value": 1.0 / dt, "ms_per_step": dt * 1e3,
+            "config": {"workload": "C3: 64^3 observations over [-7,7]^3, 8^3 inducing points, "
+                                   "EQ, optimal posterior over all N + minibatch ELBO + grads + "
+                                   "Adam(0.01)", "N": N, "M": M, "batch": B},
+            "loss_first": first, "loss_last": float(last),
+            "gemm": {"ms_per_step": ms / args.vgp_steps, "tflops": fl / (ms * 1e-3) / 1e12 if ms else None,
+                     "launches_per_step": n / args.vgp_steps}}
+
+
 def main():
     args = parse()
     import torch
@@ -129,18 +185,15 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from vgposp_amd import _lib, linalg
-    from vgposp_amd.data_generation import grid_points, grid_spacing
     from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    from vgposp_amd.workloads import placement_split
 
     shape = tuple(args.shape)
-    h = grid_spacing(shape)
     # jittered grid (seed = rank) so the selections are decided by the data, not by the exact
     # octant ties of a regular grid; this rank's split is shifted along axis 0
-    X = grid_points(shape, jitter=0.05, seed=rank)
-    X[:, 0] += rank * shape[0] * h
+    X, ls = placement_split(shape, rank)
     N = X.shape[0]
     k = args.k
-    ls = 2.0 * h
     Xd = linalg.as_device(X)
     amp_d = linalg.as_device([1.0])
     ls_d = linalg.as_device([ls])
@@ -222,6 +275,26 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
     roof.update({"kernel": dom, "launches": launches, "avg_launch_ms": ms / max(launches, 1),
                  "share_of_step": ms / (elapsed * 1e3)})
+    tr = load_traffic(args.traffic, dom, N, shape, k)
+    if tr is not None:
+        roof["traffic"] = tr["bytes_per_launch"]
+        roof["traffic_vs_algorithmic"] = tr["bytes_per_launch"] / (nbytes / max(launches, 1))
+        roof["traffic_source"] = tr["source"]
+    elif dom == "gemm_f64":
+        roof["traffic_note"] = ("null: rocprofv3 --pmc segfaults when this workload dispatches "
+                                "gemm_glds_kernel<false,false,false,true> (profiles/README.md)")
+    # the HBM-bound kernel of the placement rounds, with its PMC-measured traffic
+    ms_t, n_t, _, by_t = prof["greedy_trmv"]
+    hbm = {"kernel": "greedy_trmv", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "achieved": by_t / (ms_t * 1e-3) / 1e9 if ms_t else None, "launches": n_t,
+           "avg_launch_ms": ms_t / max(n_t, 1), "traffic": None}
+    if hbm["achieved"] is not None:
+        hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
+    trm = load_traffic(args.traffic, "greedy_trmv", N, shape, k)
+    if trm is not None and n_t:
+        hbm["traffic"] = trm["bytes_per_launch"]
+        hbm["traffic_vs_algorithmic"] = trm["bytes_per_launch"] / (by_t / n_t)
+        hbm["traffic_source"] = trm["source"]
     breakdown = {n: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[1] / args.steps,
                      "achieved": (v[2] / (v[0] * 1e-3) / 1e12 if v[2] and n == "gemm_f64" else
                                   v[3] / max(v[0], 1e-9) / 1e6),
@@ -246,10 +319,13 @@ def main():
                    "N": N, "k": k, "splits": world, "parallelism": f"split{world}"},
         "cholesky_gflops": chol_gflops,
         "roofline": roof,
+        "roofline_hbm": hbm,
         "breakdown": breakdown,
         "deterministic_selection": deterministic,
         "selected_head": [int(a) for a in g.selected[:8].cpu()],
     }
+    if world == 1 and not args.no_vgp:
+        out["vgp_c3"] = vgp_c3(args)
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, N)
     print(json.dumps(out), flush=True)

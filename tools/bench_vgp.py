@@ -18,40 +18,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from vgposp_amd import _lib
-from vgposp_amd import distributions as tfd
-from vgposp_amd import psd_kernels as tfkern
-from vgposp_amd.optimizers import AdamOptimizer
-from vgposp_amd.variables import Softplus, Variable, placeholder
-
-
-def c3_problem(n=64, m=8, half=7.0, seed=0):
-    g = np.linspace(-half, half, n)
-    X = np.stack(np.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
-    rng = np.random.default_rng(seed)
-    y = np.sum(np.exp(-X ** 2 / 20.0) * np.sin(X), axis=1) + rng.normal(0, 0.1, len(X))
-    gz = np.linspace(-half, half, m)
-    Z = np.stack(np.meshgrid(gz, gz, gz, indexing="ij"), -1).reshape(-1, 3)
-    return X, y, Z
-
-
-def build(X, y, Z, B):
-    amp = Softplus(Variable(0.54, name="amplitude"), offset=0.0)
-    ls = Softplus(Variable(0.54, name="length_scale"), offset=1e-5)
-    kernel = tfkern.ExponentiatedQuadratic(amplitude=amp, length_scale=ls)
-    noise = Softplus(Variable(0.54, name="observation_noise_variance"), offset=0.0)
-    Zv = Variable(Z, name="inducing_index_points")
-    loc, scale = tfd.VariationalGaussianProcess.optimal_variational_posterior(
-        kernel=kernel, inducing_index_points=Zv, observation_index_points=X, observations=y,
-        observation_noise_variance=noise)
-    vgp = tfd.VariationalGaussianProcess(kernel, index_points=Z[:8], inducing_index_points=Zv,
-                                         variational_inducing_observations_loc=loc,
-                                         variational_inducing_observations_scale=scale,
-                                         observation_noise_variance=noise)
-    xb = placeholder(np.float64, [B, 3], name="x_train_batch")
-    yb = placeholder(np.float64, [B], name="y_train_batch")
-    loss = vgp.variational_loss(observations=yb, observation_index_points=xb,
-                                kl_weight=float(B) / float(len(X)))
-    return AdamOptimizer(learning_rate=0.01).minimize(loss), loss, xb, yb
+from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
 
 
 def main():
@@ -63,9 +30,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    X, y, Z = c3_problem(args.n, args.m)
+    X, y, Z = vgp_c3_data(args.n, args.m)
     N, B = len(X), args.batch
-    train_op, loss, xb, yb = build(X, y, Z, B)
+    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B)
     rng = np.random.default_rng(1)
     Xd = torch.as_tensor(X, device="cuda")
     yd = torch.as_tensor(y, device="cuda")
