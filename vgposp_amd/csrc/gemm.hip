@@ -236,16 +236,14 @@ __global__ __launch_bounds__(256) void gemm_ref_kernel(GemmParams p, int vec_a, 
 #endif
 constexpr int STAGES = VGPOSP_GEMM_STAGES;
 constexpr int OPND_ELEMS = GBM * GBK;        // 2048 doubles = 16 KiB per operand per stage
-constexpr int STAGE_ELEMS = 2 * OPND_ELEMS;  // A | B
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// One 1-KiB wave-instruction ("piece" i = 0..15) of a 128-row x 16-k operand tile.
 template <bool KC>
-__device__ __forceinline__ void glds_operand(const double* base, int64_t ld, int64_t r0, int64_t k0,
-                                             int64_t R, int64_t K, double* dst, int wave, int lane) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int i = wave * 4 + j;  // wave-instruction index 0..15, 1 KiB each
+__device__ __forceinline__ void glds_piece(const double* base, int64_t ld, int64_t r0, int64_t k0,
+                                           int64_t R, int64_t K, double* dst, int i, int lane) {
+  {
     const double* src;
     if (KC) {
       const int row = 8 * i + (lane >> 3);
@@ -276,11 +274,17 @@ __device__ __forceinline__ int tri_root(int64_t id) {
   return (int)t;
 }
 
-template <bool TA, bool TB, bool TRIA, bool TRIB>
-__global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmParams p, int tiles_m, int tiles_n) {
+// BMW = 128-row A sub-tiles per workgroup: 1 -> 128x128 tiles, 4 waves, 2 workgroups per CU;
+// 2 -> 256x128 tiles, 8 waves (two per SIMD) in one workgroup: 25% fewer operand bytes per flop.
+template <bool TA, bool TB, bool TRIA, bool TRIB, int BMW>
+__global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds_kernel(
+    GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool A_KC = !TA;
   constexpr bool B_KC = TB;
-  __shared__ double smem[STAGES * STAGE_ELEMS];
+  constexpr int TBM = GBM * BMW;                       // rows per tile
+  constexpr int SE = (BMW + 1) * OPND_ELEMS;           // doubles per stage: A subs | B
+  constexpr int PPW = (16 * (BMW + 1)) / (4 * BMW);    // pieces per wave per stage (8 or 6)
+  __shared__ double smem[STAGES * SE];
 
   // Tile order.  Uniform-K launches: XCD-aware bijective remap (each XCD walks a contiguous range
   // of tiles, so neighbours share A rows / B columns in its L2).  A lower-triangular A (K range
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
     tj = local / gsize;
     if (TRIA && !TA) ti = tiles_m - 1 - ti;  // longest K ranges first
   }
-  const int64_t m0 = (int64_t)ti * GBM, n0 = (int64_t)tj * GBN;
+  const int64_t m0 = (int64_t)ti * TBM, n0 = (int64_t)tj * GBN;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
   int64_t kbeg = 0, kend = p.k;
   if (TRIA) {
     if (TA) kbeg = max(kbeg, m0);        // stored A[k][i], zero for i > k
-    else kend = min(kend, m0 + GBM);     // stored A[i][k], zero for k > i
+    else kend = min(kend, m0 + TBM);     // stored A[i][k], zero for k > i
   }
   if (TRIB) {
     if (TB) kend = min(kend, n0 + GBN);  // stored B[j][k], zero for k > j
@@ -343,11 +347,21 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
 
+  // stage layout: [A sub-tile 0 | ... | A sub-tile BMW-1 | B].  Every wave issues 4 pieces of one
+  // A sub-tile and 16 / (4 BMW) pieces of B, with no branches (measured: splitting the waves
+  // into A-loaders and B-loaders cost 10% on 8192^3).
   auto issue = [&](int t) {
-    double* st = smem + (t % STAGES) * STAGE_ELEMS;
+    double* st = smem + (t % STAGES) * SE;
     const int64_t k0 = kbeg + (int64_t)t * GBK;
-    glds_operand<A_KC>(p.A, p.lda, m0, k0, p.m, p.k, st, wave, lane);
-    glds_operand<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + OPND_ELEMS, wave, lane);
+    const int sub = wave >> 2, wa = wave & 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      glds_piece<A_KC>(p.A, p.lda, m0 + GBM * sub, k0, p.m, p.k, st + sub * OPND_ELEMS, wa * 4 + j,
+                       lane);
+    constexpr int BP = 4 / BMW;
+#pragma unroll
+    for (int j = 0; j < BP; ++j)
+      glds_piece<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + BMW * OPND_ELEMS, wave * BP + j, lane);
   };
 
 #pragma unroll
@@ -356,6 +370,7 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
 
   for (int t = 0; t < T; ++t) {
     const int after = min(T - 1 - t, STAGES - 2);  // tiles that may stay in flight
+    static_assert(STAGES == 2 || PPW == 8, "counted waits below assume 8 pieces per wave");
     if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else if (after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -363,12 +378,12 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
     __builtin_amdgcn_s_barrier();
     if (t + STAGES - 1 < T) issue(t + STAGES - 1);
 
-    const double* As = smem + (t % STAGES) * STAGE_ELEMS;
-    const double* Bs = As + OPND_ELEMS;
+    const double* As = smem + (t % STAGES) * SE + (wm >> 1) * OPND_ELEMS * (BMW - 1);
+    const double* Bs = smem + (t % STAGES) * SE + BMW * OPND_ELEMS;
     const int64_t k0 = kbeg + (int64_t)t * GBK;
     // masks only where needed: the last partial K-tile, and K-tiles that straddle the diagonal
     // of a triangular operand (k0 within 128 of the tile's first row / column)
-    const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + GBM && k0 + GBK > m0) ||
+    const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + TBM && k0 + GBK > m0) ||
                       (TRIB && k0 < n0 + GBN && k0 + GBK > n0);
 #pragma unroll
     for (int ks = 0; ks < GBK / 4; ++ks) {
@@ -376,7 +391,7 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
       double a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int r = wm * 64 + i * 16 + fr;
+        const int r = (BMW == 1 ? wm : (wm & 1)) * 64 + i * 16 + fr;  // row within the sub-tile
         a[i] = As[frag_off<A_KC>(r, k)];
       }
 #pragma unroll
@@ -429,6 +444,20 @@ __global__ __launch_bounds__(256, VGPOSP_GEMM_OCC) void gemm_glds_kernel(GemmPar
   }
 }
 
+template <int BMW>
+static void launch_glds(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn,
+                        int transa, int transb, int tri_a, int tri_b) {
+  const dim3 blk(256 * BMW);
+  if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else if (tri_b) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, true, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else if (!transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else if (!transa && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else if (transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<true, false, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
+  else hipLaunchKernelGGL((gemm_glds_kernel<true, true, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
+}
+
 // C = sum_z part[z] + beta * C over the (lower) output, fixed summation order.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int64_t m, int64_t n, int nsplit,
                                                                  const double* part, double beta,
@@ -471,6 +500,13 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(int64_t m, int64_t k, do
 }
 
 int g_fast_gemm = 1;  // 0 forces the reference kernel (tests)
+// 256x128 tiles (BMW = 2) only on request (VGPOSP_GEMM_BMW=2): measured on one box, 8192^3 NT
+// 68.0 vs 68.9 TF/s and the 65k Cholesky + inverse 3.23 vs 3.18 s against 128x128 at two
+// workgroups per CU — the fewer bytes per flop do not pay once two waves share each SIMD.
+static const bool g_bmw2 = [] {
+  const char* e = getenv("VGPOSP_GEMM_BMW");
+  return e && e[0] == '2';
+}();
 
 static bool aligned16(const void* ptr, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(ptr) % 16 == 0) && (ld % 2 == 0);
@@ -494,7 +530,10 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
   const bool tri_ok = (!tri_a && !tri_b) || (!transa && !transb && (tri_a != tri_b)) ||
                       (!transa && transb && !tri_a && tri_b) || (transa && !transb && tri_a && tri_b);
   if (va && vb && even && tri_ok && g_fast_gemm) {
-    const int tm = (int)ceil_div(m, GBM), tn = (int)ceil_div(n, GBN);
+    // 256x128 tiles (8 waves) for full-C launches with at least two rounds of workgroups, on request
+    const int bmw = (uplo_c == VGPOSP_FULL && g_bmw2 &&
+                     ceil_div(m, 2 * GBM) * ceil_div(n, GBN) >= 512) ? 2 : 1;
+    const int tm = (int)ceil_div(m, GBM * bmw), tn = (int)ceil_div(n, GBN);
     const int64_t nblk = (uplo_c == VGPOSP_LOWER) ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
     const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
     // algorithmic flops: a triangular operand halves the useful products
@@ -516,14 +555,8 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
                uplo_c == VGPOSP_LOWER ? 'L' : 'F', tri_a ? 'a' : '-', tri_b ? 'b' : '-', p.nsplit);
     ProfScope pshape(shape_name, stream, fl, 0.0, shapes && prof_on());
     dim3 g1((unsigned)(nblk * p.nsplit));
-    if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true>), g1, dim3(256), 0, stream, p, tm, tn);
-    else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
-    else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false>), g1, dim3(256), 0, stream, p, tm, tn);
-    else if (tri_b) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
-    else if (!transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
-    else if (!transa && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
-    else if (transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<true, false, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
-    else hipLaunchKernelGGL((gemm_glds_kernel<true, true, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
+    if (bmw == 2) launch_glds<2>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    else launch_glds<1>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     VG_LAUNCH_CHECK();
     if (p.nsplit > 1) {
       hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(m * n, 256)), dim3(256),
