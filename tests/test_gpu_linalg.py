@@ -83,7 +83,7 @@ def _spd(n, rng):
     return ogp.kernel_matrix("eq", X, X, 1.0, 0.7)[0] + 0.05 * np.eye(n)
 
 
-@pytest.mark.parametrize("n", [1, 5, 127, 128, 129, 300, 1000])
+@pytest.mark.parametrize("n", [1, 5, 127, 128, 129, 300, 513, 1000, 1536, 2100, 4100])
 @pytest.mark.parametrize("invert", [False, True])
 def test_cholesky(L, n, invert):
     rng = np.random.default_rng(n)

@@ -245,16 +245,43 @@ static int64_t split_point(int64_t n) {
   return NB * (nb / 2);  // >= NB for n > NB
 }
 
+// Diagonal blocks of up to NBI columns (the recursion's blocks with NB < n <= NBI) are inverted
+// as a whole right after they are factored.  The TRSMs below them are then one K <= 512
+// triangular GEMM per block instead of K = 128 GEMMs against the 128x128 leaf inverses plus the
+// updates between them, and the final inverse stops at 512 (a copy) instead of recursing to 128.
+constexpr int NBI = 4 * NB;
+
 struct Fact {
   int64_t lda;
   double* linv_all;  // ceil(n/NB) leaf inverses, NB*NB each, indexed by global column / NB
   double* work;      // trtri scratch, >= n1 * n2 doubles of the top split
+  double* xinv;      // n x NBI: block inverses, rows [col0, col0 + nb) hold block col0's (or null)
+  double* tmp;       // n x NBI: out-of-place TRSM leaf output (or null)
   double* diag_out;  // [n] or null
   int* info;
   hipStream_t s;
   double* leaf(int64_t col0) const { return linv_all + (col0 / NB) * NB * NB; }
+  double* xblk(int64_t col0) const { return xinv + col0 * NBI; }
 };
 
+// dst (n x n lower, ldd) <- src (lower, lds); zero_upper: also zero dst's strict upper triangle
+// (dst is then a full-matrix GEMM operand); otherwise dst's upper triangle is left untouched.
+__global__ void copy_lower_kernel(double* dst, int64_t ldd, const double* src, int64_t lds,
+                                  int64_t n, int zero_upper) {
+  const int64_t r = blockIdx.y;
+  for (int64_t c = threadIdx.x; c < n; c += blockDim.x) {
+    if (c <= r) dst[r * ldd + c] = src[r * lds + c];
+    else if (zero_upper) dst[r * ldd + c] = 0.0;
+  }
+}
+
+static int copy_lower(const Fact& f, double* dst, int64_t ldd, const double* src, int64_t lds,
+                      int64_t n, int zero_upper) {
+  hipLaunchKernelGGL(copy_lower_kernel, dim3(1, (unsigned)n), dim3(256), 0, f.s, dst, ldd, src, lds,
+                     n, zero_upper);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
 
 static int leaf_factor(const Fact& f, double* A, int jb, int64_t col0, int invert) {
   ProfScope ps("potrf_diag", f.s, 2.0 * jb * (double)jb * jb / 3.0, 8.0 * jb * (double)jb * 2);
@@ -266,66 +293,87 @@ static int leaf_factor(const Fact& f, double* A, int jb, int64_t col0, int inver
 }
 
 // B (m x nL, ldb) <- B L^-T, L = the nL x nL lower factor at Lp (already factored), col0 = global
-// column of L's first column (locates the leaf inverses).
+// column of L's first column (locates the leaf / block inverses).  Mirrors potrf_rec's splits, so
+// its leaves are exactly the factored leaves / blocks.
 static int trsm_rec(const Fact& f, double* B, int64_t m, int64_t ldb, const double* Lp, int64_t nL,
-                    int64_t col0) {
+                    int64_t col0, bool blocks) {
   int rc;
   if (nL <= NB) {
     // in place: the output is a single 128-wide column tile
     return gemm_launch(0, 1, m, nL, nL, 1.0, B, ldb, f.leaf(col0), NB, 0.0, B, ldb, VGPOSP_FULL, 0,
                        0, f.s);
   }
+  if (blocks && nL <= NBI) {
+    // out of place (several output column tiles read the same rows): tmp = B X^T, X lower
+    if ((rc = gemm_launch(0, 1, m, nL, nL, 1.0, B, ldb, f.xblk(col0), NBI, 0.0, f.tmp, NBI,
+                          VGPOSP_FULL, 0, 1, f.s)))
+      return rc;
+    VG_HIP(hipMemcpy2DAsync(B, ldb * sizeof(double), f.tmp, NBI * sizeof(double),
+                            nL * sizeof(double), m, hipMemcpyDeviceToDevice, f.s));
+    return 0;
+  }
   const int64_t a = split_point(nL), b = nL - a;
-  if ((rc = trsm_rec(f, B, m, ldb, Lp, a, col0))) return rc;
+  if ((rc = trsm_rec(f, B, m, ldb, Lp, a, col0, blocks))) return rc;
   // B2 -= B1 Lb^T,  Lb = L[a:, :a]
   if ((rc = gemm_launch(0, 1, m, b, a, -1.0, B, ldb, Lp + a * f.lda, f.lda, 1.0, B + a, ldb,
                         VGPOSP_FULL, 0, 0, f.s)))
     return rc;
-  return trsm_rec(f, B + a, m, ldb, Lp + a * f.lda + a, b, col0 + a);
+  return trsm_rec(f, B + a, m, ldb, Lp + a * f.lda + a, b, col0 + a, blocks);
 }
 
-static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0) {
-  if (n <= NB) return leaf_factor(f, A, (int)n, col0, 0);
-  const int64_t n1 = split_point(n), n2 = n - n1;
-  int rc;
-  double* A21 = A + n1 * f.lda;
-  double* A22 = A21 + n1;
-  if ((rc = potrf_rec(f, A, n1, col0))) return rc;
-  if ((rc = trsm_rec(f, A21, n2, f.lda, A, n1, col0))) return rc;
-  if ((rc = gemm_launch(0, 1, n2, n2, n1, -1.0, A21, f.lda, A21, f.lda, 1.0, A22, f.lda,
-                        VGPOSP_LOWER, 0, 0, f.s)))
-    return rc;
-  return potrf_rec(f, A22, n2, col0 + n1);
-}
-
-// Lower triangle of A holds L (leaf inverses saved) -> L^-1.
-static int trtri_rec(const Fact& f, double* A, int64_t n, int64_t col0) {
+// Lower triangle of A (lda) holds L (leaf inverses saved) -> L^-1.  blocks: stop at the saved
+// block inverses (n <= NBI) instead of recursing to the leaves.
+static int trtri_rec(const Fact& f, double* A, int64_t lda, int64_t n, int64_t col0, bool blocks) {
   if (n <= NB) {
     ProfScope ps("trtri_leaf", f.s, 0.0, 8.0 * NB * NB * 2);
-    hipLaunchKernelGGL(copy_leaf_kernel, dim3(NB * NB / 256), dim3(256), 0, f.s, A, f.lda, (int)n,
+    hipLaunchKernelGGL(copy_leaf_kernel, dim3(NB * NB / 256), dim3(256), 0, f.s, A, lda, (int)n,
                        f.leaf(col0));
     VG_LAUNCH_CHECK();
     return 0;
   }
+  if (blocks && n <= NBI) return copy_lower(f, A, lda, f.xblk(col0), NBI, n, 0);
+  const int64_t n1 = split_point(n), n2 = n - n1;
+  int rc;
+  double* A21 = A + n1 * lda;
+  double* A22 = A21 + n1;
+  if ((rc = trtri_rec(f, A, lda, n1, col0, blocks))) return rc;
+  if ((rc = trtri_rec(f, A22, lda, n2, col0 + n1, blocks))) return rc;
+  // W = L21 X11   (X11 lower, stored [k][j])
+  if ((rc = gemm_launch(0, 0, n2, n1, n1, 1.0, A21, lda, A, lda, 0.0, f.work, n1, VGPOSP_FULL, 0,
+                        1, f.s)))
+    return rc;
+  // X21 = -X22 W  (X22 lower, stored [i][k])
+  return gemm_launch(0, 0, n2, n1, n2, -1.0, A22, lda, f.work, n1, 0.0, A21, lda, VGPOSP_FULL, 1, 0,
+                     f.s);
+}
+
+// blocks: form the inverse of every NB < n <= NBI diagonal block (for trsm / trtri above it).
+static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0, bool blocks) {
+  if (n <= NB) return leaf_factor(f, A, (int)n, col0, 0);
+  const bool whole = blocks && n <= NBI;
   const int64_t n1 = split_point(n), n2 = n - n1;
   int rc;
   double* A21 = A + n1 * f.lda;
   double* A22 = A21 + n1;
-  if ((rc = trtri_rec(f, A, n1, col0))) return rc;
-  if ((rc = trtri_rec(f, A22, n2, col0 + n1))) return rc;
-  // W = L21 X11   (X11 lower, stored [k][j])
-  if ((rc = gemm_launch(0, 0, n2, n1, n1, 1.0, A21, f.lda, A, f.lda, 0.0, f.work, n1, VGPOSP_FULL,
-                        0, 1, f.s)))
+  const bool sub = blocks && !whole;  // inside a block the leaf-level path is used
+  if ((rc = potrf_rec(f, A, n1, col0, sub))) return rc;
+  if ((rc = trsm_rec(f, A21, n2, f.lda, A, n1, col0, sub))) return rc;
+  if ((rc = gemm_launch(0, 1, n2, n2, n1, -1.0, A21, f.lda, A21, f.lda, 1.0, A22, f.lda,
+                        VGPOSP_LOWER, 0, 0, f.s)))
     return rc;
-  // X21 = -X22 W  (X22 lower, stored [i][k])
-  return gemm_launch(0, 0, n2, n1, n2, -1.0, A22, f.lda, f.work, n1, 0.0, A21, f.lda, VGPOSP_FULL,
-                     1, 0, f.s);
+  if ((rc = potrf_rec(f, A22, n2, col0 + n1, sub))) return rc;
+  if (!whole) return 0;
+  // this block's inverse: X <- L (zero above the diagonal), then the leaf-level trtri in place
+  double* X = f.xblk(col0);
+  if ((rc = copy_lower(f, X, NBI, A, f.lda, n, 1))) return rc;
+  return trtri_rec(f, X, NBI, n, col0, false);
 }
 
 size_t potrf_ws_bytes(int64_t n) {
   const int64_t leaves = (n + NB - 1) / NB;
   const int64_t n1 = n > NB ? split_point(n) : 0;
-  return (size_t)(leaves * NB * NB + n1 * (n - n1) + 64) * sizeof(double);
+  const int64_t blk = n > NBI ? 2 * n * NBI : 0;  // xinv + tmp
+  return (size_t)(leaves * NB * NB + n1 * (n - n1) + blk + 64) * sizeof(double);
 }
 
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
@@ -337,11 +385,16 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
     attr_set = true;
   }
   const int64_t leaves = (n + NB - 1) / NB;
-  Fact f{lda, static_cast<double*>(ws), static_cast<double*>(ws) + leaves * NB * NB, diag_out,
-         info, stream};
-  int rc = potrf_rec(f, A, n, 0);
+  const int64_t n1 = n > NB ? split_point(n) : 0;
+  double* base = static_cast<double*>(ws);
+  double* work = base + leaves * NB * NB;
+  const bool blocks = n > NBI;  // a whole problem <= NBI never needs block inverses
+  double* xinv = blocks ? work + n1 * (n - n1) : nullptr;
+  double* tmp = blocks ? xinv + n * NBI : nullptr;
+  Fact f{lda, base, work, xinv, tmp, diag_out, info, stream};
+  int rc = potrf_rec(f, A, n, 0, blocks);
   if (rc || !invert) return rc;
-  return trtri_rec(f, A, n, 0);
+  return trtri_rec(f, A, lda, n, 0, blocks);
 }
 
 }  // namespace vgposp
