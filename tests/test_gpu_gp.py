@@ -138,3 +138,32 @@ def test_vgp_optimal_posterior_loss_predictive(mods, kind):
     rm, rc = ogp.vgp_predictive(kind, Xs, Z, rloc, rscale, 0.9, 0.7, 0.05)
     np.testing.assert_allclose(m, rm[0], rtol=1e-7, atol=1e-9)
     np.testing.assert_allclose(c, rc[0], rtol=1e-6, atol=1e-8)
+
+
+def test_gprm_posterior_sampling_at_scale(mods):
+    """GPRM joint samples over a 50 x 50 prediction mesh (M = 2,500, as
+    gp_functions.create_meshgrid / tf_gp_regression_model build it, gp_functions.py:262-297),
+    conditioned on 512 observations: posterior mean / covariance vs the oracle, the M x M
+    posterior Cholesky vs numpy, and the sample moments."""
+    import torch
+    dist, psd, gpf, _ = mods
+    X, y = _data(512, 2, seed=8)
+    Xs = gpf.create_meshgrid(np.linspace(-2, 2, 50), np.linspace(-2, 2, 50))
+    k = psd.ExponentiatedQuadratic(0.9, 0.6)
+    gprm = gpf.tf_gp_regression_model(k, Xs, X, y, 0.05, 0.0)
+    mean, cov = gprm._posterior()
+    rm, rc = ogp.gprm_mean_cov("eq", Xs, X, y, 0.9, 0.6, 0.05, 0.0)
+    np.testing.assert_allclose(mean[0].cpu().numpy(), rm[0], rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(cov[0].cpu().numpy(), rc[0], rtol=1e-6, atol=1e-9)
+    C = cov.clone()
+    C.diagonal(dim1=-2, dim2=-1).add_(gprm.jitter)
+    from vgposp_amd import linalg
+    L, _, _ = linalg.cholesky_(C, invert=False, check=True)
+    Lref = np.linalg.cholesky(rc[0] + gprm.jitter * np.eye(2500))
+    got = torch.tril(L[0]).cpu().numpy()
+    np.testing.assert_allclose(got, Lref, rtol=1e-5, atol=1e-8 * np.abs(Lref).max())
+    s = gprm.sample(4000, seed=3).cpu().numpy()  # [S, M]
+    assert s.shape == (4000, 2500) and np.isfinite(s).all()
+    emp_mean = s.mean(0)
+    sd = np.sqrt(np.diag(rc[0]) + gprm.jitter)
+    assert np.all(np.abs(emp_mean - rm[0]) < 5 * sd / np.sqrt(4000) + 1e-9)
