@@ -32,8 +32,8 @@ int main() {
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     long long st[16]; hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
-    printf("kernel %.1f us | panel-chol %lld | panel-inv %lld | trsm %lld | syrk %lld | inverse %lld | out %lld (memtime ticks)\n",
-           ms * 1e3, st[0], st[1], st[2], st[3], st[4], st[5]);
+    printf("kernel %.1f us | panel %lld | trsm %lld | syrk %lld | inverse %lld | out %lld (memtime ticks)\n",
+           ms * 1e3, st[1], st[2], st[3], st[4], st[5]);
   }
   return 0;
 }

@@ -61,6 +61,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Broadcast a double from a (wave-uniform) lane.
+__device__ __forceinline__ double readlane_d(double v, int src) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ int leaf_tri_root(int t) {
   int r = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
   while ((r + 1) * (r + 2) / 2 <= t) ++r;
@@ -95,71 +102,72 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   for (int p = 0; p < NP; ++p) {
     const int c0 = p * LW;
     if (wave == 0) {
-      // unblocked Cholesky of the 16x16 diagonal block
-      for (int c = 0; c < LW; ++c) {
-        const int cc = c0 + c;
-        const double d = L[cc * LP2 + cc];
-        const double piv = sqrt(d), inv = 1.0 / piv;
-        if (lane > c && lane < LW) L[(c0 + lane) * LP2 + cc] *= inv;
-        if (lane == 0) {
-          if (!(d > 0.0) && cc < jb) atomicCAS(info, 0, (int)(col0 + cc + 1));
-          rdiag[cc] = inv;
-          L[cc * LP2 + cc] = piv;
-        }
-        wave_sync();
-        for (int e = lane; e < LW * LW; e += 64) {
-          const int r = e >> 4, s2 = e & 15;
-          if (s2 > c && s2 <= r) L[(c0 + r) * LP2 + c0 + s2] -= L[(c0 + r) * LP2 + cc] * L[(c0 + s2) * LP2 + cc];
-        }
-        wave_sync();
+      // 16x16 diagonal block in registers, symmetric (both triangles kept): lane (g, j) holds
+      // D[4g + q][j], q = 0..3.  Column step c: pivot by readlane, scale column c and row c,
+      // rank-1 update of the trailing block; the inverse X = L^-1 is eliminated alongside
+      // ([L | I] -> [I | L^-1]: row c /= L[c][c], rows r > c -= L[r][c] row c) with the same
+      // broadcasts.  No LDS traffic and no barriers inside the 16 steps.
+      const int j = lane & 15, g = lane >> 4;
+      double D[4], X[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 4 * g + q;
+        D[q] = r >= j ? L[(c0 + r) * LP2 + c0 + j] : L[(c0 + j) * LP2 + c0 + r];
+        X[q] = r == j ? 1.0 : 0.0;
       }
-      STAMP_ADD(0, ts);
-      ts = STAMP_NOW();
-      // its inverse by rows, X[r][j] = -(sum_{k=j}^{r-1} L[r][k] X[k][j]) / L[r][r], stored
-      // transposed in the block's upper part; 4 lanes split each sum
-      {
-        const int j = lane & 15, part = lane >> 4;
-        for (int r = 1; r < LW; ++r) {
-          double acc = 0.0;
-          if (j < r) {
-            for (int k = j + part; k < r; k += 4)
-              acc += L[(c0 + r) * LP2 + c0 + k] * (k == j ? rdiag[c0 + j] : L[(c0 + j) * LP2 + c0 + k]);
-          }
-          acc += __shfl_xor(acc, 16, 64);
-          acc += __shfl_xor(acc, 32, 64);
-          if (part == 0 && j < r) L[(c0 + j) * LP2 + c0 + r] = -acc * rdiag[c0 + r];
-          wave_sync();
+#pragma unroll
+      for (int c = 0; c < LW; ++c) {
+        const int gc = c >> 2, qc = c & 3;
+        const double d = readlane_d(D[qc], gc * 16 + c);
+        const double piv = sqrt(d), inv = 1.0 / piv;
+        if (lane == 0) {
+          if (!(d > 0.0) && c0 + c < jb) atomicCAS(info, 0, (int)(col0 + c0 + c + 1));
+          rdiag[c0 + c] = inv;
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * g + q;
+          if (j == c) D[q] = r == c ? piv : (r > c ? D[q] * inv : D[q]);
+          else if (r == c && j > c) D[q] *= inv;
+          if (r == c) X[q] *= inv;
+        }
+        const double xc = __shfl(X[qc], gc * 16 + j, 64);  // X[c][j]
+        const double dc = __shfl(D[qc], gc * 16 + j, 64);  // D[c][j] = L[j][c] (j > c)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * g + q;
+          const double a = __shfl(D[q], (lane & 0x30) | c, 64);  // L[r][c]
+          if (r > c) {
+            if (j > c) D[q] -= a * dc;
+            X[q] -= a * xc;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 4 * g + q;
+        if (r >= j) L[(c0 + r) * LP2 + c0 + j] = D[q];
+        if (r > j) L[(c0 + j) * LP2 + c0 + r] = X[q];  // X strictly lower, stored transposed
       }
     }
     __syncthreads();
     STAMP_ADD(1, ts);
     ts = STAMP_NOW();
-    // rows below: P[r][j] = sum_{k <= j} L[r][c0+k] X[j][k]; thread (j = t & 15) owns rows
-    // c0 + 16 + (t >> 4) + 16 q, whose sums run as independent chains over k
-    constexpr int NQ = (NB - LW) / 16;
-    {
-      const int j = t & 15, rb = c0 + LW + (t >> 4);
-      double acc[NQ];
+    // rows below: P = A_panel X^T on MFMA, one 16-row tile (K = 16) per wave-iteration; each
+    // tile is read and rewritten by one wave only
+    const int nrt = (JP - c0 - LW) / 16;
+    for (int tt = wave; tt < nrt; tt += 4) {
+      const int r0 = c0 + LW + 16 * tt;
+      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int r = rb + 16 * q;
-        acc[q] = r < JP ? L[r * LP2 + c0 + j] * rdiag[c0 + j] : 0.0;
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int k = 4 * s4 + fk;
+        const double a = L[(r0 + fr) * LP2 + c0 + k];
+        const double b = fr > k ? L[(c0 + k) * LP2 + c0 + fr] : (fr == k ? rdiag[c0 + k] : 0.0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
       }
-      for (int k = 0; k < j; ++k) {
-        const double xk = L[(c0 + k) * LP2 + c0 + j];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int r = rb + 16 * q;
-          if (r < JP) acc[q] += L[r * LP2 + c0 + k] * xk;
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int r = rb + 16 * q;
-        if (r < JP) L[r * LP2 + c0 + j] = acc[q];
-      }
+      for (int reg = 0; reg < 4; ++reg) L[(r0 + fk + 4 * reg) * LP2 + c0 + fr] = acc[reg];
     }
     __syncthreads();
     STAMP_ADD(2, ts);
