@@ -171,3 +171,20 @@ def test_reference_training_graph_trajectory(torch_dev):
     rm, _ = ogp.vgp_predictive("eq", index_points, th[3:, None], rloc, rscale, sp(th[0]),
                                1e-5 + sp(th[1]), sp(th[2]))
     np.testing.assert_allclose(mean, rm[0], rtol=1e-6, atol=1e-8)
+
+
+@pytest.mark.parametrize("m,k,transa", [(512, 262144, False), (37, 5000, False), (300, 40000, True),
+                                        (2049, 700, True), (1, 3, True)])
+def test_gemv_split_and_transposed(torch_dev, m, k, transa):
+    """n == 1 products: split-K row GEMV and the transposed (column) GEMV."""
+    from vgposp_amd import linalg
+    torch = torch_dev
+    rng = np.random.default_rng(m + k)
+    A = rng.normal(size=(k, m) if transa else (m, k))
+    x = rng.normal(size=(k, 1))
+    y0 = rng.normal(size=(m, 1))
+    y = torch.as_tensor(y0, device="cuda").clone()
+    linalg.gemm(torch.as_tensor(A, device="cuda"), torch.as_tensor(x, device="cuda"), y, alpha=0.5,
+                beta=-2.0, transa=transa)
+    ref = 0.5 * ((A.T if transa else A) @ x) - 2.0 * y0
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-11, atol=1e-10)

@@ -10,6 +10,9 @@ import argparse
 import json
 import os
 import sys
+
+if "--shapes" in sys.argv:
+    os.environ["VGPOSP_PROF_SHAPES"] = "1"
 import time
 
 import numpy as np
@@ -28,6 +31,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32768)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--shapes", action="store_true", help="per-shape GEMM / per-kernel dump")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     X, y, Z = vgp_c3_data(args.n, args.m)
@@ -56,6 +60,11 @@ def main():
             prof[name] = {"ms_per_step": ms / args.steps, "launches_per_step": launches / args.steps,
                           "TFLOP/s": flops / (ms * 1e-3) / 1e12 if flops else None,
                           "GB/s": nbytes / (ms * 1e-3) / 1e9}
+    if args.shapes:
+        d = _lib.prof_dump()
+        for name, (ms, n, fl, _) in sorted(d.items(), key=lambda kv: -kv[1][0])[:30]:
+            tf = fl / (ms * 1e-3) / 1e12 if fl and ms else 0.0
+            print(f"{name:44s} {ms / args.steps:8.3f} ms/step {n / args.steps:6.1f} x {tf:6.1f} TF/s")
     _lib.prof_enable(False)
     M = Z.shape[0]
     print(json.dumps({"N": N, "M": M, "batch": B, "ms_per_step": dt * 1e3,

@@ -499,6 +499,73 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(int64_t m, int64_t k, do
   }
 }
 
+// Split-K GEMV: wave (row r, split z) writes part[z][r]; then gemv_reduce.  For a few rows and a
+// long K (c = Kzx y of the VGP: 512 rows x 262,144) one wave per row leaves most CUs idle.
+__global__ __launch_bounds__(256) void gemv_rows_split_kernel(int64_t m, int64_t k, int64_t kchunk,
+                                                              const double* A, int64_t lda,
+                                                              const double* x, int64_t incx,
+                                                              double* part) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= m) return;
+  const int64_t k0 = (int64_t)blockIdx.y * kchunk, k1 = min(k, k0 + kchunk);
+  const double* row = A + r * lda;
+  double s0 = 0.0, s1 = 0.0;
+  int64_t c = k0 + lane;
+  for (; c + 64 < k1; c += 128) {
+    s0 += row[c] * x[c * incx];
+    s1 += row[c + 64] * x[(c + 64) * incx];
+  }
+  if (c < k1) s0 += row[c] * x[c * incx];
+  const double s = wave_sum(s0 + s1);
+  if (lane == 0) part[(int64_t)blockIdx.y * m + r] = s;
+}
+
+// y = alpha A^T x (+ beta y) with A stored k x m (row-major): thread j owns output j, the k rows
+// it walks are read coalesced across the workgroup.  Split over k when part != null.
+__global__ __launch_bounds__(256) void gemv_t_kernel(int64_t m, int64_t k, int64_t kchunk,
+                                                     double alpha, const double* A, int64_t lda,
+                                                     const double* x, int64_t incx, double beta,
+                                                     double* y, int64_t incy, double* part) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= m) return;
+  const int64_t k0 = (int64_t)blockIdx.y * kchunk, k1 = min(k, k0 + kchunk);
+  double s0 = 0.0, s1 = 0.0;
+  int64_t c = k0;
+  for (; c + 1 < k1; c += 2) {
+    s0 += A[c * lda + j] * x[c * incx];
+    s1 += A[(c + 1) * lda + j] * x[(c + 1) * incx];
+  }
+  if (c < k1) s0 += A[c * lda + j] * x[c * incx];
+  if (part) {
+    part[(int64_t)blockIdx.y * m + j] = s0 + s1;
+  } else {
+    double v = alpha * (s0 + s1);
+    if (beta != 0.0) v += beta * y[j * incy];
+    y[j * incy] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void gemv_reduce_kernel(int64_t m, int nsplit, const double* part,
+                                                          double alpha, double beta, double* y,
+                                                          int64_t incy) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= m) return;
+  double s = 0.0;
+  for (int z = 0; z < nsplit; ++z) s += part[(int64_t)z * m + r];
+  double v = alpha * s;
+  if (beta != 0.0) v += beta * y[r * incy];
+  y[r * incy] = v;
+}
+
+// splits for the n == 1 paths: about 2048 waves in flight, >= 2048 (rows) / 256 (transposed)
+// K elements per split
+static int gemv_splits(int64_t m, int64_t k, int transa) {
+  int64_t s = transa ? ceil_div(2048 * 64, std::max<int64_t>(m, 1)) : ceil_div(2048, m);
+  s = std::min<int64_t>(s, transa ? k / 256 : k / 2048);
+  return (int)std::max<int64_t>(std::min<int64_t>(s, 4096), 1);
+}
+
 int g_fast_gemm = 1;  // 0 forces the reference kernel (tests)
 // 256x128 tiles (BMW = 2) only on request (VGPOSP_GEMM_BMW=2): measured on one box, 8192^3 NT
 // 68.0 vs 68.9 TF/s and the 65k Cholesky + inverse 3.23 vs 3.18 s against 128x128 at two
@@ -517,11 +584,30 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
                       double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
                       double* part, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
-  if (n == 1 && !transa && !tri_a && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
+  if (n == 1 && !tri_a && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
     ProfScope ps("gemv_f64", stream, 2.0 * (double)m * k, 8.0 * ((double)m * k + k + 2.0 * m));
-    hipLaunchKernelGGL(gemv_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, stream, m, k,
-                       alpha, A, lda, B, transb ? 1 : ldb, beta, C, ldc);
+    const int64_t incx = transb ? 1 : ldb;
+    const int S = (nsplit > 1 && part != nullptr) ? nsplit : 1;
+    const int64_t kchunk = ceil_div(k, S);
+    if (!transa) {
+      if (S == 1) {
+        hipLaunchKernelGGL(gemv_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, stream, m,
+                           k, alpha, A, lda, B, incx, beta, C, ldc);
+      } else {
+        hipLaunchKernelGGL(gemv_rows_split_kernel, dim3((unsigned)ceil_div(m, 4), (unsigned)S),
+                           dim3(256), 0, stream, m, k, kchunk, A, lda, B, incx, part);
+      }
+    } else {
+      hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)ceil_div(m, 256), (unsigned)S), dim3(256), 0,
+                         stream, m, k, kchunk, alpha, A, lda, B, incx, beta, C, ldc,
+                         S > 1 ? part : nullptr);
+    }
     VG_LAUNCH_CHECK();
+    if (S > 1) {
+      hipLaunchKernelGGL(gemv_reduce_kernel, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, stream,
+                         m, S, part, alpha, beta, C, ldc);
+      VG_LAUNCH_CHECK();
+    }
     return 0;
   }
   GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr};
@@ -586,7 +672,8 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
 
 // Split count for a launch with few output tiles and a long K: enough workgroups for 256 CUs
 // (about two per CU), each split at least 512 deep.
-static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c) {
+static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa = 0) {
+  if (n == 1 && uplo_c == VGPOSP_FULL) return gemv_splits(m, k, transa);
   const int64_t tm = ceil_div(m, GBM), tn = ceil_div(n, GBN);
   const int64_t nblk = uplo_c == VGPOSP_LOWER ? tm * (tm + 1) / 2 : tm * tn;
   int64_t s = ceil_div(512, nblk);
@@ -600,7 +687,10 @@ extern "C" size_t vgposp_gemm_splitk_workspace_bytes(int64_t m, int64_t n, int64
                                                      int splits) {
   using namespace vgposp;
   if (m <= 0 || n <= 0 || k <= 0) return 0;
-  if (splits <= 0) splits = auto_splits(m, n, k, uplo_c);
+  // the GEMV paths pick their split count by transa, which this query does not take: size for
+  // the larger of the two
+  if (splits <= 0)
+    splits = std::max(auto_splits(m, n, k, uplo_c, 0), auto_splits(m, n, k, uplo_c, 1));
   return splits > 1 ? 8 * (size_t)splits * m * n : 0;
 }
 
@@ -622,7 +712,7 @@ extern "C" int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, 
   VG_CHECK_ARG(ldc >= (n > 0 ? n : 1), 13);
   VG_CHECK_ARG(uplo_c == VGPOSP_FULL || (uplo_c == VGPOSP_LOWER && m == n), 14);
   if (m == 0 || n == 0) return 0;
-  if (splits <= 0) splits = k > 0 ? auto_splits(m, n, k, uplo_c) : 1;
+  if (splits <= 0) splits = k > 0 ? auto_splits(m, n, k, uplo_c, transa) : 1;
   if (splits > 1) {
     const size_t need = 8 * (size_t)splits * m * n;
     if (ws == nullptr || ws_bytes < need) {
