@@ -676,7 +676,10 @@ static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa =
   if (n == 1 && uplo_c == VGPOSP_FULL) return gemv_splits(m, k, transa);
   const int64_t tm = ceil_div(m, GBM), tn = ceil_div(n, GBN);
   const int64_t nblk = uplo_c == VGPOSP_LOWER ? tm * (tm + 1) / 2 : tm * tn;
-  int64_t s = ceil_div(512, nblk);
+  // one full round of workgroup slots (256 CUs x 2 workgroups): the splits all run the same K
+  // length, so a round that overflows by a few workgroups costs a whole second round (measured:
+  // 10 lower tiles x 52 splits = 520 > 512 ran as slowly as the 16-tile full product)
+  int64_t s = 512 / nblk;
   s = std::min<int64_t>(s, k / 512);
   return (int)std::max<int64_t>(s, 1);
 }
