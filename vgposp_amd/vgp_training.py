@@ -56,9 +56,13 @@ def kernel_vjp(kind, X1, X2, amp, ls, Kbar, u=None, w=None, want_x1bar=True):
     return grad, X1bar
 
 
-def _chol_inv(A):
-    """(L^-1 with explicit zeros above the diagonal, sum log diag L) of an SPD [M, M] (copied)."""
-    Li, ld, _ = linalg.cholesky_(A.clone(), invert=True, check=True)
+def _chol_inv(A, infos=None):
+    """(L^-1 with explicit zeros above the diagonal, sum log diag L) of an SPD [M, M] (copied).
+    With ``infos`` (a list) the device status is appended for a later check instead of being
+    synchronised on here."""
+    Li, ld, info = linalg.cholesky_(A.clone(), invert=True, check=infos is None)
+    if infos is not None:
+        infos.append(info)
     return torch.tril(Li), torch.sum(torch.log(ld))
 
 
@@ -98,6 +102,7 @@ class VGPObjective:
         self.trace_adjoint = bool(trace_adjoint)
         self.group = group
         self._Kzx = None
+        self._side = None
 
     def _allreduce(self, t):
         """Sum over the data-parallel group (host-staged for gloo, in place on device for RCCL)."""
@@ -126,9 +131,35 @@ class VGPObjective:
         st = self._forward_posterior(Z, a, l, s)
         return st["m"], st["A"]
 
-    def _forward_posterior(self, Z, a, l, s):
+    def _kzz_factors(self, Kzz, s, infos):
+        """The three Cholesky + inverse factorizations that need only Kzz (Kzz + jitter I for the
+        VGP, Kzz + (noise + 1e-6) I for the KL prior, Kzz itself for log|det A|), enqueued on a
+        side stream so that their latency-bound leaves overlap the Kzx assembly and the split-K
+        Kzx Kzx^T on the main stream.  The caller waits on the returned stream before use."""
+        main = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        side = self._side
+        side.wait_stream(main)
+        Kzz.record_stream(side)
+        M = Kzz.shape[0]
+        with torch.cuda.stream(side):
+            I = torch.eye(M, dtype=F64, device=Kzz.device)
+            Lzi, _ = _chol_inv(Kzz + self.j * I, infos)
+            Lpi, logdetLp = _chol_inv(Kzz + (s + 1e-6) * I, infos)
+            Lki, logdetLk = _chol_inv(Kzz, infos)
+            out = dict(Lzi=Lzi, Kzj_inv=_spd_inv(Lzi), Lpi=Lpi, logdetLp=logdetLp,
+                       Kp_inv=_spd_inv(Lpi), Kzz_inv=_spd_inv(Lki), logdetLk=logdetLk)
+        for t in out.values():
+            t.record_stream(main)
+        for t in infos:
+            t.record_stream(main)
+        return out, side
+
+    def _forward_posterior(self, Z, a, l, s, infos=None, side=False):
         M = Z.shape[0]
         Kzz = linalg.kernel_matrix(self.kind, Z, Z, a, l)[0]
+        fac = self._kzz_factors(Kzz, s, infos) if side else None
         Kzx = self._kzx(Z, a, l)
         red = torch.empty(M * M + M, dtype=F64, device=Z.device)
         P0 = red[:M * M].view(M, M)
@@ -140,12 +171,15 @@ class VGPObjective:
         c = c.reshape(-1)
         Sinv = Kzz + P0 / s
         Sinv.diagonal().add_(self.pj)
-        Li, logdetL = _chol_inv(Sinv)
+        Li, logdetL = _chol_inv(Sinv, infos)
         t = linalg.gemm(Li, linalg.gemm(Li, _col(c), tri_a=True), transa=True, tri_a=True)
         m = linalg.gemm(Kzz, t).reshape(-1) / s
         A = linalg.gemm(Li, Kzz, tri_a=True)
-        return dict(Kzz=Kzz, Kzx=Kzx, P0=P0, c=c, Li=Li, logdetL=logdetL, t=t.reshape(-1), m=m,
-                    A=A)
+        st = dict(Kzz=Kzz, Kzx=Kzx, P0=P0, c=c, Li=Li, logdetL=logdetL, t=t.reshape(-1), m=m, A=A)
+        if fac is not None:
+            torch.cuda.current_stream().wait_stream(fac[1])
+            st.update(fac[0])
+        return st
 
     def loss_and_grads(self, Z, amp, ls, noise, Xb, yb, kl_weight, want_grads=True):
         """-> (loss, d/damp, d/dls, d/dnoise, d/dZ [M, d]) as 0-d / [M, d] device tensors."""
@@ -157,16 +191,16 @@ class VGPObjective:
         a, l, s = (linalg.as_device(v).reshape(()) for v in (amp, ls, noise))
         j, w = self.j, float(kl_weight)
         M, nb = Z.shape[0], yb.numel()
-        I = torch.eye(M, dtype=F64, device=Z.device)
         s_h = float(s)  # host copy for GEMM alphas (the one sync of a step)
-        st = self._forward_posterior(Z, a, l, s)
+        infos = []      # Cholesky statuses, checked once at the end
+        st = self._forward_posterior(Z, a, l, s, infos, side=True)
         Kzz, Kzx, P0, c, Li, logdetL, t, m, A = (st[k] for k in
                                                  ("Kzz", "Kzx", "P0", "c", "Li", "logdetL", "t",
                                                   "m", "A"))
         Kzb = linalg.kernel_matrix(self.kind, Z, Xb, a, l)[0]
         # ---- variational loss ----
-        Lzi, _ = _chol_inv(Kzz + j * I)
-        Kzj_inv = _spd_inv(Lzi)
+        Lzi, Kzj_inv, Lpi, logdetLp, Kp_inv, Kzz_inv, logdetLk = (
+            st[k] for k in ("Lzi", "Kzj_inv", "Lpi", "logdetLp", "Kp_inv", "Kzz_inv", "logdetLk"))
         v = linalg.gemm(Kzj_inv, _col(m))
         r = yb - linalg.gemm(Kzb, v, transa=True).reshape(-1)
         v = v.reshape(-1)
@@ -177,14 +211,14 @@ class VGPObjective:
         H = linalg.gemm(Kzj_inv, Kzb)
         R = linalg.gemm(A, H, transa=self.trace_adjoint)
         T = 0.5 * (nb * a * a - torch.sum(G * G) + torch.sum(R * R)) / s
-        Lpi, logdetLp = _chol_inv(Kzz + (s + 1e-6) * I)
-        Lki, logdetLk = _chol_inv(Kzz)
         logdetA = 2.0 * logdetLk - logdetL
         PA = linalg.gemm(Lpi, A, tri_a=True)
         qm = linalg.gemm(Lpi, _col(m), tri_a=True)
         KL = logdetLp - logdetA + 0.5 * (-M + torch.sum(PA * PA) + torch.sum(qm * qm))
         E = obs - T - w * KL
         if not want_grads:
+            for info in infos:
+                linalg.check_info(info)
             return -E, None, None, None, None
         # ---- reverse pass (d E) ----
         mu_b = r / s2
@@ -205,7 +239,6 @@ class VGPObjective:
         KH = linalg.gemm(Kzj_inv, H_b)
         Kzb_b += KH
         linalg.gemm(KH, H, Kzz_b, alpha=-1.0, beta=1.0, transb=True)
-        Kp_inv = _spd_inv(Lpi)
         QA = linalg.gemm(Kp_inv, A)
         qv = linalg.gemm(Kp_inv, _col(m)).reshape(-1)
         A_b -= w * QA
@@ -215,7 +248,7 @@ class VGPObjective:
         Kp_b *= -0.5 * w
         Kzz_b += Kp_b
         s_b = s_b + torch.trace(Kp_b)
-        Kzz_b += w * _spd_inv(Lki)
+        Kzz_b += w * Kzz_inv
         Sinv_b = (-0.5 * w) * _spd_inv(Li)
         Kzz_b += torch.outer(m_b, t) / s
         t_b = linalg.gemm(Kzz, _col(m_b)) / s
@@ -242,6 +275,8 @@ class VGPObjective:
         a_b = a_b + 0.5 * g1[0] + g2[0] + g3[0]
         l_b = 0.5 * g1[1] + g2[1] + g3[1]
         Z_b = Zb1 + Zb2 + Zb3
+        for info in infos:
+            linalg.check_info(info)
         return -E, -a_b, -l_b, -s_b, -Z_b
 
 
