@@ -680,8 +680,16 @@ static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa =
   // length, so a round that overflows by a few workgroups costs a whole second round (measured:
   // 10 lower tiles x 52 splits = 520 > 512 ran as slowly as the 16-tile full product)
   int64_t s = 512 / nblk;
-  s = std::min<int64_t>(s, k / 512);
+  // long K: splits at least 512 deep.  Short K (few output tiles, e.g. the M x M products of the
+  // VGP step, 16 tiles of a 512^3 product on 16 CUs): up to 8 splits, at least 64 deep — each
+  // split's 128x128 partial costs 256 KB of HBM traffic, about the time of 64 K-steps on one CU.
+  const int64_t deep = k / 512;
+  s = std::min<int64_t>(s, deep >= 8 ? deep : std::min<int64_t>(8, k / 64));
   return (int)std::max<int64_t>(s, 1);
+}
+
+int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa) {
+  return auto_splits(m, n, k, uplo_c, transa);
 }
 
 }  // namespace vgposp

@@ -20,23 +20,26 @@
 
 namespace vgposp {
 
-int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
-                const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
-                double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, hipStream_t stream);
+int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                      const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                      double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
+                      double* part, hipStream_t stream);
+int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa);
 
 constexpr int NB = 128;        // leaf size (== GEMM tile, so trsm leaves are in place)
 
 
 // ---------------------------------------------------------------------------------------------
 // Blocked leaf: Cholesky + inverse of a jb x jb (jb <= 128) block in LDS, one workgroup of 4 waves.
-// Panels of 16 columns: wave 0 factors the 16x16 diagonal block (and inverts it) with wave-level
-// syncs only; all waves apply it to the rows below (TRSM by the block inverse) and update the
-// trailing lower triangle with v_mfma_f64_16x16x4f64 (16x16 tiles, K = 16).  The inverse is then
-// formed block row by block row:  X_ij = -X_ii * sum_{k=j}^{i-1} L_ik X_kj  (two MFMA chains per
-// 16x16 tile, the first chain's accumulator feeding the second directly as its B operand).
-// ~3 barriers per panel instead of 3 per column.  X (strictly lower) lives transposed in the
-// upper triangle of the LDS image, diag(X) = 1 / diag(L) in rdiag.  jb is padded to a multiple of
-// 16 with an identity block.
+// Left-looking over 16-column panels: all waves bring the panel up to date with MFMA
+// (A[c0:, c0:c0+16] -= L[c0:, :c0] L[c0:c0+16, :c0]^T), then wave 0 factors the whole tall panel
+// in registers (a lane per row, broadcasts through SGPRs), which also solves the rows below the
+// diagonal block — two barriers per panel.  The inverse follows: the 16x16 diagonal blocks by
+// forward substitution (all blocks at once), then X_ij = -X_ii * sum_{k=j}^{i-1} L_ik X_kj as
+// independent block-column chains per wave (two MFMA chains per 16x16 tile, the first chain's
+// accumulator feeding the second directly as its B operand).  X (strictly lower) lives transposed
+// in the upper triangle of the LDS image, diag(X) = 1 / diag(L) in rdiag.  jb is padded to a
+// multiple of 16 with an identity block.
 // ---------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
@@ -75,9 +78,49 @@ __device__ __forceinline__ int leaf_tri_root(int t) {
   return r;
 }
 
-// X[R][C] of the inverse (lower, R >= C) from the LDS image.
-__device__ __forceinline__ double xval(const double* L, const double* rdiag, int R, int C) {
-  return R > C ? L[C * LP2 + R] : (R == C ? rdiag[R] : 0.0);
+// 1 / sqrt(d) from the hardware estimate plus two Newton steps (full fp64 precision, not
+// correctly rounded): 7 dependent VALU ops instead of the ~25 of sqrt() followed by 1.0 / x.
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const double e = fma(-d * r, r, 1.0);
+    r = fma(0.5 * r, e, r);
+  }
+  return r;
+}
+
+// Register panel factor, one wave: lane l owns panel rows r0 = c0 + l (D0) and, when the panel is
+// taller than 64, r1 = c0 + 64 + l (D1); register k holds column c0 + k.  The pivot and
+// L[c0 + k][c0 + c] (k > c) are broadcast through SGPRs (v_readlane), so a column costs one
+// reciprocal square root and 2 (15 - c) readlanes + FMAs with no LDS traffic and no barrier.  Rows
+// below the 16x16 diagonal block come out solved (the panel TRSM is part of the elimination).
+// (Measured alternative: 64-bit DPP row_newbcast folded into v_fmac_f64 is ~12x slower on gfx950.)
+template <bool TALL>
+__device__ __forceinline__ void leaf_panel(double (&D0)[LW], double (&D1)[LW], int lane, int c0,
+                                           int jb, int64_t col0, int* info, double* rdiag) {
+  double my_d = 1.0, my_inv = 1.0;  // lane c < 16 keeps column c's pivot and its reciprocal
+#pragma unroll
+  for (int c = 0; c < LW; ++c) {
+    const double d = readlane_d(D0[c], c);
+    const double inv = rsqrt_nr(d), piv = d * inv;
+    if (lane == c) {
+      my_d = d;
+      my_inv = inv;
+    }
+    D0[c] = lane == c ? piv : D0[c] * inv;
+    if (TALL) D1[c] *= inv;
+#pragma unroll
+    for (int k = c + 1; k < LW; ++k) {
+      const double lkc = readlane_d(D0[c], k);  // L[c0 + k][c0 + c]
+      D0[k] -= D0[c] * lkc;
+      if (TALL) D1[k] -= D1[c] * lkc;
+    }
+  }
+  // statuses and reciprocals once per panel (no branches inside the column steps)
+  const unsigned long long bad = __ballot(lane < LW && c0 + lane < jb && !(my_d > 0.0));
+  if (lane < LW) rdiag[c0 + lane] = my_inv;
+  if (lane == 0 && bad) atomicCAS(info, 0, (int)(col0 + c0 + __ffsll((long long)bad)));
 }
 
 __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int64_t lda, int jb,
@@ -86,141 +129,142 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
                                                                   int* info, int64_t stride_a) {
   extern __shared__ double L[];  // [NB][LP2]
   __shared__ double rdiag[NB];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ double XD[(NB / LW) * LW * LW];  // dense diagonal blocks of L^-1
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   A += blockIdx.x * stride_a;
   info += blockIdx.x;
   if (diag_out) diag_out += (int64_t)blockIdx.x * jb;
   const int JP = (jb + LW - 1) & ~(LW - 1), NP = JP / LW;
-  for (int e = t; e < JP * JP; e += LEAF_THREADS) {
-    const int r = e / JP, c = e - r * JP;
-    if (c <= r) L[r * LP2 + c] = r < jb ? A[(int64_t)r * lda + c] : (r == c ? 1.0 : 0.0);
+  for (int e = t; e < NB * NB; e += LEAF_THREADS) {
+    const int r = e / NB, c = e % NB;
+    if (r < JP && c <= r) L[r * LP2 + c] = r < jb ? A[(int64_t)r * lda + c] : (r == c ? 1.0 : 0.0);
   }
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
   long long ts = STAMP_NOW();
 
+  // Left-looking over 16-column panels:
+  //   A[c0:, c0:c0+16] -= L[c0:, :c0] L[c0:c0+16, :c0]^T   (MFMA, 16-row tiles over the 4 waves)
+  //   factor the tall panel A[c0:, c0:c0+16] in wave 0's registers (leaf_panel)
   for (int p = 0; p < NP; ++p) {
     const int c0 = p * LW;
-    if (wave == 0) {
-      // 16x16 diagonal block in registers, symmetric (both triangles kept): lane (g, j) holds
-      // D[4g + q][j], q = 0..3.  Column step c: pivot by readlane, scale column c and row c,
-      // rank-1 update of the trailing block; the inverse X = L^-1 is eliminated alongside
-      // ([L | I] -> [I | L^-1]: row c /= L[c][c], rows r > c -= L[r][c] row c) with the same
-      // broadcasts.  No LDS traffic and no barriers inside the 16 steps.
-      const int j = lane & 15, g = lane >> 4;
-      double D[4], X[4];
+    if (p > 0) {
+      const int nrt = NP - p;
+      for (int tt = wave; tt < nrt; tt += 4) {
+        const int r0 = c0 + LW * tt;
+        dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int k0 = 0; k0 < c0; k0 += LW) {  // c0 is a multiple of 16: loads issued together
+          double a[4], b[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 4 * g + q;
-        D[q] = r >= j ? L[(c0 + r) * LP2 + c0 + j] : L[(c0 + j) * LP2 + c0 + r];
-        X[q] = r == j ? 1.0 : 0.0;
-      }
-#pragma unroll
-      for (int c = 0; c < LW; ++c) {
-        const int gc = c >> 2, qc = c & 3;
-        const double d = readlane_d(D[qc], gc * 16 + c);
-        const double piv = sqrt(d), inv = 1.0 / piv;
-        if (lane == 0) {
-          if (!(d > 0.0) && c0 + c < jb) atomicCAS(info, 0, (int)(col0 + c0 + c + 1));
-          rdiag[c0 + c] = inv;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 4 * g + q;
-          if (j == c) D[q] = r == c ? piv : (r > c ? D[q] * inv : D[q]);
-          else if (r == c && j > c) D[q] *= inv;
-          if (r == c) X[q] *= inv;
-        }
-        const double xc = __shfl(X[qc], gc * 16 + j, 64);  // X[c][j]
-        const double dc = __shfl(D[qc], gc * 16 + j, 64);  // D[c][j] = L[j][c] (j > c)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = 4 * g + q;
-          const double a = __shfl(D[q], (lane & 0x30) | c, 64);  // L[r][c]
-          if (r > c) {
-            if (j > c) D[q] -= a * dc;
-            X[q] -= a * xc;
+          for (int s4 = 0; s4 < 4; ++s4) {
+            a[s4] = L[(r0 + fr) * LP2 + k0 + 4 * s4 + fk];
+            b[s4] = L[(c0 + fr) * LP2 + k0 + 4 * s4 + fk];
           }
-        }
-      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = 4 * g + q;
-        if (r >= j) L[(c0 + r) * LP2 + c0 + j] = D[q];
-        if (r > j) L[(c0 + j) * LP2 + c0 + r] = X[q];  // X strictly lower, stored transposed
+          for (int s4 = 0; s4 < 4; ++s4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], b[s4], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) L[(r0 + fk + 4 * reg) * LP2 + c0 + fr] -= acc[reg];
+      }
+      __syncthreads();
+    }
+    STAMP_ADD(3, ts);
+    ts = STAMP_NOW();
+    if (wave == 0) {
+      const int r0 = c0 + lane, r1 = c0 + 64 + lane;
+      const bool tall = JP - c0 > 64;
+      double D0[LW], D1[LW];
+#pragma unroll
+      for (int k = 0; k < LW; ++k) {
+        D0[k] = r0 < JP ? L[r0 * LP2 + c0 + k] : 0.0;
+        D1[k] = (tall && r1 < JP) ? L[r1 * LP2 + c0 + k] : 0.0;
+      }
+      if (tall) leaf_panel<true>(D0, D1, lane, c0, jb, col0, info, rdiag);
+      else leaf_panel<false>(D0, D1, lane, c0, jb, col0, info, rdiag);
+#pragma unroll
+      for (int k = 0; k < LW; ++k) {
+        if (r0 < JP && (lane >= LW || k <= lane)) L[r0 * LP2 + c0 + k] = D0[k];
+        if (tall && r1 < JP) L[r1 * LP2 + c0 + k] = D1[k];
       }
     }
     __syncthreads();
     STAMP_ADD(1, ts);
     ts = STAMP_NOW();
-    // rows below: P = A_panel X^T on MFMA, one 16-row tile (K = 16) per wave-iteration; each
-    // tile is read and rewritten by one wave only
-    const int nrt = (JP - c0 - LW) / 16;
-    for (int tt = wave; tt < nrt; tt += 4) {
-      const int r0 = c0 + LW + 16 * tt;
-      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  }
+
+  if (invert || linv) {
+    // Diagonal-block inverses, all blocks at once: lane group fk of wave w inverts block
+    // b = 4 fk + w, lane fr its column by forward substitution (x[k] = 0 for k < column).  Kept
+    // dense in XD (zeros above the diagonal) for branch-free MFMA operands, and strictly lower
+    // transposed into the block's upper triangle of L for the output pass.
+    {
+      const int b = 4 * fk + wave, j = fr, b0 = b * LW;
+      if (b < NP) {
+        double x[LW];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int k = 4 * s4 + fk;
-        const double a = L[(r0 + fr) * LP2 + c0 + k];
-        const double b = fr > k ? L[(c0 + k) * LP2 + c0 + fr] : (fr == k ? rdiag[c0 + k] : 0.0);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        for (int i = 0; i < LW; ++i) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < i; ++k) s += L[(b0 + i) * LP2 + b0 + k] * x[k];
+          x[i] = i < j ? 0.0 : (i == j ? rdiag[b0 + i] : -rdiag[b0 + i] * s);
+          XD[b * LW * LW + i * LW + j] = x[i];
+        }
+#pragma unroll
+        for (int i = 0; i < LW; ++i)
+          if (i > j) L[(b0 + j) * LP2 + b0 + i] = x[i];
       }
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) L[(r0 + fk + 4 * reg) * LP2 + c0 + fr] = acc[reg];
     }
     __syncthreads();
     STAMP_ADD(2, ts);
     ts = STAMP_NOW();
-    // trailing lower triangle -= P P^T on MFMA, 16x16 tiles
-    const int NT = NP - p - 1, ntile = NT * (NT + 1) / 2;
-    for (int tt = wave; tt < ntile; tt += 4) {
-      const int ti = leaf_tri_root(tt), tj = tt - ti * (ti + 1) / 2;
-      const int r0 = c0 + LW + LW * ti, s0 = c0 + LW + LW * tj;
-      dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+    // Off-diagonal blocks, one block column per chain: X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj for
+    // i = j+1 .. NP-1 depends only on block column j, so a wave owns whole columns (j and
+    // NP-1-j: balanced work for NP <= 8) and needs wave-level ordering only.
+    for (int h = 0; h < 2; ++h) {
+      const int j = h == 0 ? wave : NP - 1 - wave;
+      if (wave > NP - 1 - wave || (h == 1 && j == wave)) break;
+      const int j0 = j * LW;
+      const double* xjj = XD + j * LW * LW;
+      for (int i = j + 1; i < NP; ++i) {
+        const int i0 = i * LW;
+        const double* li = L + (i0 + fr) * LP2 + fk;
+        dbl4 S = {0.0, 0.0, 0.0, 0.0};
+        {
+          double a[4], b[4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const double a = L[(r0 + fr) * LP2 + c0 + 4 * s4 + fk];
-        const double b = L[(s0 + fr) * LP2 + c0 + 4 * s4 + fk];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-      }
+          for (int s4 = 0; s4 < 4; ++s4) {
+            a[s4] = li[j0 + 4 * s4];
+            b[s4] = xjj[(4 * s4 + fk) * LW + fr];
+          }
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int row = r0 + fk + 4 * reg, col = s0 + fr;
-        if (ti != tj || col <= row) L[row * LP2 + col] -= acc[reg];
+          for (int s4 = 0; s4 < 4; ++s4)
+            S = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], b[s4], S, 0, 0, 0);
+        }
+        const double* xcol = L + (j0 + fr) * LP2 + fk;  // X_kj, k > j, stored transposed
+        for (int k0 = j0 + LW; k0 < i0; k0 += LW) {
+          double a[4], b[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            a[s4] = li[k0 + 4 * s4];
+            b[s4] = xcol[k0 + 4 * s4];
+          }
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            S = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], b[s4], S, 0, 0, 0);
+        }
+        const double* xii = XD + i * LW * LW + fr * LW + fk;
+        dbl4 X = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          X = __builtin_amdgcn_mfma_f64_16x16x4f64(xii[4 * s4], S[s4], X, 0, 0, 0);
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) L[(j0 + fr) * LP2 + i0 + fk + 4 * reg] = -X[reg];
+        wave_sync();
       }
     }
     __syncthreads();
-    STAMP_ADD(3, ts);
-    ts = STAMP_NOW();
-  }
-
-  if (invert || linv) {
-    for (int i = 1; i < NP; ++i) {
-      const int i0 = i * LW;
-      for (int j = wave; j < i; j += 4) {
-        const int j0 = j * LW;
-        dbl4 S = {0.0, 0.0, 0.0, 0.0};
-        for (int k = j; k < i; ++k) {
-          const int k0 = k * LW;
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const double a = L[(i0 + fr) * LP2 + k0 + 4 * s4 + fk];
-            const double b = xval(L, rdiag, k0 + 4 * s4 + fk, j0 + fr);
-            S = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, S, 0, 0, 0);
-          }
-        }
-        dbl4 X = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const double a = xval(L, rdiag, i0 + fr, i0 + 4 * s4 + fk);
-          X = __builtin_amdgcn_mfma_f64_16x16x4f64(a, S[s4], X, 0, 0, 0);
-        }
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) L[(j0 + fr) * LP2 + i0 + fk + 4 * reg] = -X[reg];
-      }
-      __syncthreads();
-    }
   }
   STAMP_ADD(4, ts);
   ts = STAMP_NOW();
@@ -267,10 +311,27 @@ struct Fact {
   double* tmp;       // n x NBI: out-of-place TRSM leaf output (or null)
   double* diag_out;  // [n] or null
   int* info;
+  double* part;      // split-K partials, PART_ELEMS doubles (or null)
   hipStream_t s;
   double* leaf(int64_t col0) const { return linv_all + (col0 / NB) * NB * NB; }
   double* xblk(int64_t col0) const { return xinv + col0 * NBI; }
 };
+
+// Split-K partials for the recursion's few-tile GEMMs (the 128..1024 levels: a 128^3 TRSM or SYRK
+// is one 128x128 tile, i.e. one CU): up to 8 splits, bounded by this many doubles (16 MB).
+constexpr int64_t PART_ELEMS = 2 << 20;
+
+// C = alpha op(A) op(B) + beta C with the split count of vgposp_gemm_splitk, reduced to what the
+// partials area holds.  In-place operands (C also read as A) are safe: the split kernels only
+// write the partials, the reduction writes C after all of them.
+static int pgemm(const Fact& f, int transa, int transb, int64_t m, int64_t n, int64_t k,
+                 double alpha, const double* A, int64_t lda, const double* B, int64_t ldb,
+                 double beta, double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b) {
+  int sp = f.part ? gemm_auto_splits(m, n, k, uplo_c, transa) : 1;
+  while (sp > 1 && (int64_t)sp * m * n > PART_ELEMS) --sp;
+  return gemm_launch_split(transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, uplo_c,
+                           tri_a, tri_b, sp, sp > 1 ? f.part : nullptr, f.s);
+}
 
 // dst (n x n lower, ldd) <- src (lower, lds); zero_upper: also zero dst's strict upper triangle
 // (dst is then a full-matrix GEMM operand); otherwise dst's upper triangle is left untouched.
@@ -308,13 +369,12 @@ static int trsm_rec(const Fact& f, double* B, int64_t m, int64_t ldb, const doub
   int rc;
   if (nL <= NB) {
     // in place: the output is a single 128-wide column tile
-    return gemm_launch(0, 1, m, nL, nL, 1.0, B, ldb, f.leaf(col0), NB, 0.0, B, ldb, VGPOSP_FULL, 0,
-                       0, f.s);
+    return pgemm(f, 0, 1, m, nL, nL, 1.0, B, ldb, f.leaf(col0), NB, 0.0, B, ldb, VGPOSP_FULL, 0, 0);
   }
   if (blocks && nL <= NBI) {
     // out of place (several output column tiles read the same rows): tmp = B X^T, X lower
-    if ((rc = gemm_launch(0, 1, m, nL, nL, 1.0, B, ldb, f.xblk(col0), NBI, 0.0, f.tmp, NBI,
-                          VGPOSP_FULL, 0, 1, f.s)))
+    if ((rc = pgemm(f, 0, 1, m, nL, nL, 1.0, B, ldb, f.xblk(col0), NBI, 0.0, f.tmp, NBI,
+                    VGPOSP_FULL, 0, 1)))
       return rc;
     VG_HIP(hipMemcpy2DAsync(B, ldb * sizeof(double), f.tmp, NBI * sizeof(double),
                             nL * sizeof(double), m, hipMemcpyDeviceToDevice, f.s));
@@ -323,8 +383,8 @@ static int trsm_rec(const Fact& f, double* B, int64_t m, int64_t ldb, const doub
   const int64_t a = split_point(nL), b = nL - a;
   if ((rc = trsm_rec(f, B, m, ldb, Lp, a, col0, blocks))) return rc;
   // B2 -= B1 Lb^T,  Lb = L[a:, :a]
-  if ((rc = gemm_launch(0, 1, m, b, a, -1.0, B, ldb, Lp + a * f.lda, f.lda, 1.0, B + a, ldb,
-                        VGPOSP_FULL, 0, 0, f.s)))
+  if ((rc = pgemm(f, 0, 1, m, b, a, -1.0, B, ldb, Lp + a * f.lda, f.lda, 1.0, B + a, ldb,
+                  VGPOSP_FULL, 0, 0)))
     return rc;
   return trsm_rec(f, B + a, m, ldb, Lp + a * f.lda + a, b, col0 + a, blocks);
 }
@@ -347,12 +407,10 @@ static int trtri_rec(const Fact& f, double* A, int64_t lda, int64_t n, int64_t c
   if ((rc = trtri_rec(f, A, lda, n1, col0, blocks))) return rc;
   if ((rc = trtri_rec(f, A22, lda, n2, col0 + n1, blocks))) return rc;
   // W = L21 X11   (X11 lower, stored [k][j])
-  if ((rc = gemm_launch(0, 0, n2, n1, n1, 1.0, A21, lda, A, lda, 0.0, f.work, n1, VGPOSP_FULL, 0,
-                        1, f.s)))
+  if ((rc = pgemm(f, 0, 0, n2, n1, n1, 1.0, A21, lda, A, lda, 0.0, f.work, n1, VGPOSP_FULL, 0, 1)))
     return rc;
   // X21 = -X22 W  (X22 lower, stored [i][k])
-  return gemm_launch(0, 0, n2, n1, n2, -1.0, A22, lda, f.work, n1, 0.0, A21, lda, VGPOSP_FULL, 1, 0,
-                     f.s);
+  return pgemm(f, 0, 0, n2, n1, n2, -1.0, A22, lda, f.work, n1, 0.0, A21, lda, VGPOSP_FULL, 1, 0);
 }
 
 // blocks: form the inverse of every NB < n <= NBI diagonal block (for trsm / trtri above it).
@@ -366,8 +424,8 @@ static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0, bool blo
   const bool sub = blocks && !whole;  // inside a block the leaf-level path is used
   if ((rc = potrf_rec(f, A, n1, col0, sub))) return rc;
   if ((rc = trsm_rec(f, A21, n2, f.lda, A, n1, col0, sub))) return rc;
-  if ((rc = gemm_launch(0, 1, n2, n2, n1, -1.0, A21, f.lda, A21, f.lda, 1.0, A22, f.lda,
-                        VGPOSP_LOWER, 0, 0, f.s)))
+  if ((rc = pgemm(f, 0, 1, n2, n2, n1, -1.0, A21, f.lda, A21, f.lda, 1.0, A22, f.lda,
+                  VGPOSP_LOWER, 0, 0)))
     return rc;
   if ((rc = potrf_rec(f, A22, n2, col0 + n1, sub))) return rc;
   if (!whole) return 0;
@@ -381,7 +439,8 @@ size_t potrf_ws_bytes(int64_t n) {
   const int64_t leaves = (n + NB - 1) / NB;
   const int64_t n1 = n > NB ? split_point(n) : 0;
   const int64_t blk = n > NBI ? 2 * n * NBI : 0;  // xinv + tmp
-  return (size_t)(leaves * NB * NB + n1 * (n - n1) + blk + 64) * sizeof(double);
+  const int64_t part = n > NB ? PART_ELEMS : 0;
+  return (size_t)(leaves * NB * NB + n1 * (n - n1) + blk + part + 64) * sizeof(double);
 }
 
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
@@ -399,7 +458,8 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
   const bool blocks = n > NBI;  // a whole problem <= NBI never needs block inverses
   double* xinv = blocks ? work + n1 * (n - n1) : nullptr;
   double* tmp = blocks ? xinv + n * NBI : nullptr;
-  Fact f{lda, base, work, xinv, tmp, diag_out, info, stream};
+  double* part = n > NB ? work + n1 * (n - n1) + (blocks ? 2 * n * NBI : 0) : nullptr;
+  Fact f{lda, base, work, xinv, tmp, diag_out, info, part, stream};
   int rc = potrf_rec(f, A, n, 0, blocks);
   if (rc || !invert) return rc;
   return trtri_rec(f, A, lda, n, 0, blocks);
