@@ -57,6 +57,32 @@ def test_gemm(L, ta, tb, m, n, k):
     np.testing.assert_allclose(C.cpu().numpy(), -1.5 * opA @ opB + 0.5 * C0, rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("ta,tb,tri_a,tri_b", [(0, 0, 0, 0), (0, 1, 0, 0), (1, 0, 0, 0),
+                                               (1, 1, 0, 0), (0, 0, 1, 0), (0, 0, 0, 1),
+                                               (0, 1, 0, 1), (1, 0, 1, 1)])
+def test_gemm_many_tiles(L, ta, tb, tri_a, tri_b):
+    """Enough output tiles (>= 512 of 256x128) for the wide-tile kernel when it is enabled
+    (VGPOSP_GEMM_BMW=2); ragged m / n / k exercise the clamped loads and masks."""
+    m, n, k = 4352, 4224, 200
+    if tri_a or tri_b:
+        k = m if tri_a else n
+    rng = np.random.default_rng(ta + 2 * tb + 4 * tri_a + 8 * tri_b)
+    A = rng.standard_normal((k, m) if ta else (m, k))
+    B = rng.standard_normal((n, k) if tb else (k, n))
+    opA = A.T if ta else A
+    opB = B.T if tb else B
+    if tri_a:  # the stored matrix is lower triangular
+        opA = np.tril(A).T if ta else np.tril(A)
+    if tri_b:
+        opB = np.tril(B).T if tb else np.tril(B)
+    C0 = rng.standard_normal((m, n))
+    C = L.as_device(C0.copy())
+    L.gemm(A, B, C, alpha=0.75, beta=-0.5, transa=bool(ta), transb=bool(tb), tri_a=bool(tri_a),
+           tri_b=bool(tri_b))
+    ref = 0.75 * opA @ opB - 0.5 * C0
+    np.testing.assert_allclose(C.cpu().numpy(), ref, rtol=1e-11, atol=1e-10)
+
+
 def test_gemm_asymmetric_layout(L):
     """A = I with an asymmetric B catches a transposed C/D fragment map."""
     A = np.eye(16)

@@ -274,17 +274,24 @@ __device__ __forceinline__ int tri_root(int64_t id) {
   return (int)t;
 }
 
-// BMW = 128-row A sub-tiles per workgroup: 1 -> 128x128 tiles, 4 waves, 2 workgroups per CU;
-// 2 -> 256x128 tiles, 8 waves (two per SIMD) in one workgroup: 25% fewer operand bytes per flop.
+// BMW = 128-row A sub-tiles per workgroup, always 4 waves in a 2x2 grid:
+//   1 -> 128x128 tiles, 64x64 per wave (4x4 fragments), STAGES-deep ring, 2 workgroups per CU;
+//   2 -> 256x128 tiles, 128x64 per wave (8x4 fragments, 128 accumulators in AGPRs), 3-stage ring
+//        (144 KiB), 1 workgroup per CU: a third fewer LDS fragment reads and operand bytes per
+//        MFMA, latency hidden by the deeper ring instead of a second workgroup.
 template <bool TA, bool TB, bool TRIA, bool TRIB, int BMW>
-__global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds_kernel(
+__global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds_kernel(
     GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool A_KC = !TA;
   constexpr bool B_KC = TB;
   constexpr int TBM = GBM * BMW;                       // rows per tile
+  constexpr int WROWS = 64 * BMW;                      // rows per wave
+  constexpr int FI = 4 * BMW;                          // 16-row fragments per wave
+  constexpr int NST = BMW == 1 ? STAGES : 3;           // ring depth
   constexpr int SE = (BMW + 1) * OPND_ELEMS;           // doubles per stage: A subs | B
-  constexpr int PPW = (16 * (BMW + 1)) / (4 * BMW);    // pieces per wave per stage (8 or 6)
-  __shared__ double smem[STAGES * SE];
+  constexpr int PPW = 4 * (BMW + 1);                   // pieces per wave per stage (8 or 12)
+  constexpr bool SPREAD = NST >= 3;                    // next-tile loads between the MFMAs
+  __shared__ double smem[NST * SE];
 
   // Tile order.  Uniform-K launches: XCD-aware bijective remap (each XCD walks a contiguous range
   // of tiles, so neighbours share A rows / B columns in its L2).  A lower-triangular A (K range
@@ -341,45 +348,57 @@ __global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gem
   const int T = (int)((kend - kbeg + GBK - 1) / GBK);
   const bool partial_last = ((kend - kbeg) % GBK) != 0;
 
-  dbl4 acc[4][4];
+  dbl4 acc[FI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
 
-  // stage layout: [A sub-tile 0 | ... | A sub-tile BMW-1 | B].  Every wave issues 4 pieces of one
-  // A sub-tile and 16 / (4 BMW) pieces of B, with no branches (measured: splitting the waves
-  // into A-loaders and B-loaders cost 10% on 8192^3).
-  auto issue = [&](int t) {
-    double* st = smem + (t % STAGES) * SE;
+  // stage layout: [A sub-tile 0 | ... | A sub-tile BMW-1 | B].  Every wave issues 4 pieces of each
+  // A sub-tile and 4 of B, with no branches (measured: splitting the waves into A-loaders and
+  // B-loaders cost 10% on 8192^3).
+  // piece q (0 .. PPW-1) of this wave for K-tile t: q / 4 = operand (A sub-tiles, then B)
+  auto issue_piece = [&](int t, int q) {
+    double* st = smem + (t % NST) * SE;
     const int64_t k0 = kbeg + (int64_t)t * GBK;
-    const int sub = wave >> 2, wa = wave & 3;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      glds_piece<A_KC>(p.A, p.lda, m0 + GBM * sub, k0, p.m, p.k, st + sub * OPND_ELEMS, wa * 4 + j,
+    const int op = q >> 2, j = q & 3;
+    if (op < BMW)
+      glds_piece<A_KC>(p.A, p.lda, m0 + GBM * op, k0, p.m, p.k, st + op * OPND_ELEMS, wave * 4 + j,
                        lane);
-    constexpr int BP = 4 / BMW;
+    else
+      glds_piece<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + BMW * OPND_ELEMS, wave * 4 + j, lane);
+  };
+  auto issue = [&](int t) {
 #pragma unroll
-    for (int j = 0; j < BP; ++j)
-      glds_piece<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + BMW * OPND_ELEMS, wave * BP + j, lane);
+    for (int q = 0; q < PPW; ++q) issue_piece(t, q);
   };
 
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
+  for (int s = 0; s < NST - 1; ++s)
     if (s < T) issue(s);
 
   for (int t = 0; t < T; ++t) {
-    const int after = min(T - 1 - t, STAGES - 2);  // tiles that may stay in flight
-    static_assert(STAGES == 2 || PPW == 8, "counted waits below assume 8 pieces per wave");
-    if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int after = min(T - 1 - t, NST - 2);  // tiles that may stay in flight
+    static_assert(PPW == 8 || PPW == 12, "counted waits below assume 8 or 12 pieces per wave");
+    if (PPW == 8) {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (t + STAGES - 1 < T) issue(t + STAGES - 1);
+    // 3-stage ring: the next K-tile's pieces are spread over the k-slices below, between MFMAs
+    // (issued back to back they park the wave for their issue cost; 8192^3 NT 63.3 -> 65.7 TF/s).
+    // 2-stage ring: issued here, as early as possible — the tile is needed one K-step later.
+    const bool more = t + NST - 1 < T;
+    if (!SPREAD && more) issue(t + NST - 1);
 
-    const double* As = smem + (t % STAGES) * SE + (wm >> 1) * OPND_ELEMS * (BMW - 1);
-    const double* Bs = smem + (t % STAGES) * SE + BMW * OPND_ELEMS;
+    const double* As = smem + (t % NST) * SE + (BMW == 1 ? 0 : wm * OPND_ELEMS);
+    const double* Bs = smem + (t % NST) * SE + BMW * OPND_ELEMS;
     const int64_t k0 = kbeg + (int64_t)t * GBK;
     // masks only where needed: the last partial K-tile, and K-tiles that straddle the diagonal
     // of a triangular operand (k0 within 128 of the tile's first row / column)
@@ -388,10 +407,10 @@ __global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gem
 #pragma unroll
     for (int ks = 0; ks < GBK / 4; ++ks) {
       const int k = ks * 4 + fk;
-      double a[4], b[4];
+      double a[FI], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = (BMW == 1 ? wm : (wm & 1)) * 64 + i * 16 + fr;  // row within the sub-tile
+      for (int i = 0; i < FI; ++i) {
+        const int r = (BMW == 1 ? wm * 64 : 0) + i * 16 + fr;  // row within the sub-tile
         a[i] = As[frag_off<A_KC>(r, k)];
       }
 #pragma unroll
@@ -402,8 +421,8 @@ __global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gem
       if (mask) {
         const int64_t gk = k0 + k;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t gm = m0 + wm * 64 + i * 16 + fr;
+        for (int i = 0; i < FI; ++i) {
+          const int64_t gm = m0 + wm * WROWS + i * 16 + fr;
           if (gk >= kend || (TRIA && (TA ? gm > gk : gk > gm))) a[i] = 0.0;
         }
 #pragma unroll
@@ -412,8 +431,12 @@ __global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gem
           if (gk >= kend || (TRIB && (TB ? gk > gn : gn > gk))) b[j] = 0.0;
         }
       }
+      if (SPREAD && more) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int q = ks * (PPW / 4); q < (ks + 1) * (PPW / 4); ++q) issue_piece(t + NST - 1, q);
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
@@ -422,13 +445,13 @@ __global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gem
 
   const bool lower = p.uplo_c == VGPOSP_LOWER;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < FI; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int64_t col = n0 + wn * 64 + j * 16 + fr;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + fk + 4 * r;
+        const int64_t row = m0 + wm * WROWS + i * 16 + fk + 4 * r;
         if (row < p.m && col < p.n && (!lower || col <= row)) {
           if (p.nsplit > 1) {
             p.part[(int64_t)zsplit * p.m * p.n + row * p.n + col] = p.alpha * acc[i][j][r];
@@ -447,7 +470,7 @@ __global__ __launch_bounds__(256 * BMW, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gem
 template <int BMW>
 static void launch_glds(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn,
                         int transa, int transb, int tri_a, int tri_b) {
-  const dim3 blk(256 * BMW);
+  const dim3 blk(256);
   if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true, BMW>), g1, blk, 0, stream, p, tm, tn);
   else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true, BMW>), g1, blk, 0, stream, p, tm, tn);
   else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false, BMW>), g1, blk, 0, stream, p, tm, tn);
