@@ -47,7 +47,8 @@ def parse():
     p.add_argument("--cpu-shape", type=int, nargs=3, default=[8, 8, 8])
     p.add_argument("--cpu-k", type=int, default=2)
     p.add_argument("--no-potrf", action="store_true", help="skip the separate potrf GF/s run")
-    p.add_argument("--no-vgp", action="store_true", help="skip the C3 VGP training line")
+    p.add_argument("--no-vgp", action="store_true", help="skip the C3 / C5 VGP training lines")
+    p.add_argument("--no-c2", action="store_true", help="skip the C2 assembly + potrf line")
     p.add_argument("--vgp-steps", type=int, default=10)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r1.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
@@ -136,15 +137,19 @@ def load_traffic(path, kernel, N, shape, k):
     return {"bytes_per_launch": kern["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
 
 
-def vgp_c3(args):
-    """Config C3: VGP training steps/s at N = 64^3, M = 512, minibatch 32,768 —
-    optimal posterior over all N + minibatch ELBO + analytic gradient + Adam, on this GPU."""
+def vgp_line(args, which="c3"):
+    """Config C3 or C5: VGP training steps/s on this GPU — optimal posterior over all
+    N + minibatch ELBO + analytic gradient + Adam(0.01), minibatch N / 8.
+      C3: N = 64^3 observations over [-7, 7]^3, M = 8^3, 3-D.
+      C5: N = 65,536 uniform over [-2, 2]^5, M = 4^5 = 1,024, 5-D (computed in fp64, at or above
+          the fp32 + refinement the config names)."""
     import torch
 
     from vgposp_amd import _lib
-    from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
-    X, y, Z = vgp_c3_data()
-    N, M, B = len(X), len(Z), 32768
+    from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph, vgp_c5_data
+    X, y, Z = vgp_c3_data() if which == "c3" else vgp_c5_data()
+    N, M = len(X), len(Z)
+    B = N // 8
     train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B)
     Xd = torch.as_tensor(X, device="cuda")
     yd = torch.as_tensor(y, device="cuda")
@@ -161,13 +166,57 @@ def vgp_c3(args):
     dt = (time.perf_counter() - t0) / args.vgp_steps
     ms, n, fl, _ = _lib.prof_query("gemm_f64")
     _lib.prof_enable(False)
+    desc = ("C3: 64^3 observations over [-7,7]^3, 8^3 inducing points" if which == "c3" else
+            "C5: 65,536 observations U[-2,2]^5, 4^5 inducing points, fp64")
     return {"metric": "VGP ELBO Adam steps/sec", "value": 1.0 / dt, "ms_per_step": dt * 1e3,
-            "config": {"workload": "C3: 64^3 observations over [-7,7]^3, 8^3 inducing points, "
-                                   "EQ, optimal posterior over all N + minibatch ELBO + grads + "
-                                   "Adam(0.01)", "N": N, "M": M, "batch": B},
+            "config": {"workload": desc + ", EQ, optimal posterior over all N + minibatch ELBO + "
+                                          "grads + Adam(0.01)", "N": N, "M": M, "d": X.shape[1],
+                       "batch": B},
             "loss_first": first, "loss_last": float(last),
             "gemm": {"ms_per_step": ms / args.vgp_steps, "tflops": fl / (ms * 1e-3) / 1e12 if ms else None,
                      "launches_per_step": n / args.vgp_steps}}
+
+
+def c2_line(reps=2):
+    """Config C2: N = 32,768 (32^3 grid) K assembly (lower triangle + noise on the
+    diagonal, GB/s of algorithmic bytes 4 n (n + 1) + 8 d n) and the fp64 Cholesky (GF/s of
+    n^3 / 3), each the best of ``reps`` runs after a warm-up."""
+    import torch
+
+    from vgposp_amd import linalg
+    from vgposp_amd.workloads import c2_data
+    X, ls = c2_data()
+    n, d = X.shape
+    Xd = linalg.as_device(X)
+    A = torch.empty((1, n, n), dtype=torch.float64, device="cuda")
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def assemble():
+        linalg.kernel_matrix("eq", Xd, None, 1.0, ls, diag_shift=0.01 + 1e-6, lower=True, out=A)
+
+    def timed(fn):
+        best = None
+        for _ in range(reps):
+            assemble()
+            torch.cuda.synchronize()
+            ev[0].record()
+            fn()
+            ev[1].record()
+            torch.cuda.synchronize()
+            t = ev[0].elapsed_time(ev[1]) * 1e-3
+            best = t if best is None else min(best, t)
+        return best
+
+    assemble()
+    linalg.cholesky_(A[0], check=True)  # warm-up (and the PD check)
+    t_k = timed(assemble)
+    t_c = timed(lambda: linalg.cholesky_(A[0], check=False))
+    del A
+    torch.cuda.empty_cache()
+    return {"config": {"workload": "C2: 32^3 grid over [-2,2]^3, EQ amp 1 ls 2h, noise 1e-2+1e-6",
+                       "N": n},
+            "assembly_ms": t_k * 1e3, "assembly_gbps": (4.0 * n * (n + 1) + 8.0 * d * n) / t_k / 1e9,
+            "potrf_ms": t_c * 1e3, "potrf_gflops": n ** 3 / 3.0 / t_c / 1e9}
 
 
 def main():
@@ -325,7 +374,10 @@ def main():
         "selected_head": [int(a) for a in g.selected[:8].cpu()],
     }
     if world == 1 and not args.no_vgp:
-        out["vgp_c3"] = vgp_c3(args)
+        out["vgp_c3"] = vgp_line(args, "c3")
+        out["vgp_c5"] = vgp_line(args, "c5")
+    if world == 1 and not args.no_c2:
+        out["c2"] = c2_line()
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args, N)
     print(json.dumps(out), flush=True)

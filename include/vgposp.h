@@ -130,11 +130,12 @@ int vgposp_index_taper(double* C, int64_t n, int64_t ldc, int64_t I0, int64_t I1
                        double beta, double threshold, int uplo, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
- * Blocked right-looking Cholesky, lower, in place.  Replaces tf.linalg.cholesky inside
- * tfd.GaussianProcess.log_prob / GPRM / VGP (gp_functions.py:166-172, main.py:105,
- * 3D_sin_wave.py:172) and is the O(N^3) core of the dense greedy placement.
+ * Recursive Cholesky, lower, in place (128x128 leaves in LDS, everything else fp64 MFMA GEMMs).
+ * Replaces tf.linalg.cholesky inside tfd.GaussianProcess.log_prob / GPRM / VGP
+ * (gp_functions.py:166-172, main.py:105, 3D_sin_wave.py:172) and is the O(N^3) core of the dense
+ * greedy placement.
  *   invert = 0: lower triangle of A <- L with A = L L^T.
- *   invert = 1: lower triangle of A <- L^-1 (block Gauss-Jordan fused into the same sweep).
+ *   invert = 1: lower triangle of A <- L^-1 (recursive triangular inverse after the factor).
  * The strictly upper triangle of A is never read or written (it keeps Sigma for the greedy
  * nominators).  diag_out ([batch][n], or NULL) receives diag(L) (log-det).  info: [batch] int32.
  * ws must hold vgposp_potrf_workspace_bytes(n).
@@ -142,6 +143,17 @@ int vgposp_index_taper(double* C, int64_t n, int64_t ldc, int64_t I0, int64_t I1
 size_t vgposp_potrf_workspace_bytes(int64_t n);
 int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t stride, int batch, int invert,
                        double* diag_out, int* info, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Left-side triangular solve with a factor from vgposp_potrf_lower(invert = 0), in place on B:
+ *   trans = 0:  B (n x nrhs, ldb) <- L^-1 B        trans = 1:  B <- L^-T B
+ * Replaces tf.linalg.triangular_solve(L, ...) inside tfd.GaussianProcess.log_prob and the
+ * GPRM posterior (gp_functions.py:166-172, 283-297; SURVEY §8(b) vgposp_trsm_lower).  The
+ * strictly upper triangle of L is never read.  ws: vgposp_trsm_workspace_bytes(n, nrhs).
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_trsm_workspace_bytes(int64_t n, int64_t nrhs);
+int vgposp_trsm_lower(const double* L, int64_t n, int64_t ldl, int trans, double* B, int64_t nrhs,
+                      int64_t ldb, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * GP log marginal likelihood from the inverted factor.  Replaces

@@ -156,3 +156,22 @@ def test_lml_and_grad(L, kind, n):
     np.testing.assert_allclose(g[:, 0], ga, rtol=1e-8)
     np.testing.assert_allclose(g[:, 1], gl, rtol=1e-8)
     np.testing.assert_allclose(g[:, 2], gn, rtol=1e-8)
+
+
+@pytest.mark.parametrize("n", [1, 5, 128, 129, 300, 1000, 2100])
+@pytest.mark.parametrize("nrhs", [1, 7, 300])
+@pytest.mark.parametrize("trans", [False, True])
+def test_trsm(L, n, nrhs, trans):
+    """vgposp_trsm_lower vs a dense solve with the numpy factor: L^-1 B and L^-T B (the two
+    triangular solves of tfd.GaussianProcess.log_prob / GPRM)."""
+    rng = np.random.default_rng(n + 3 * nrhs + int(trans))
+    S = _spd(n, rng)
+    Lf = np.linalg.cholesky(S)
+    Lstore = Lf + np.triu(rng.standard_normal((n, n)), 1) * 1e3  # garbage above the diagonal
+    B = rng.standard_normal((n, nrhs))
+    X = L.trsm(Lstore, B, trans=trans).cpu().numpy()
+    ref = np.linalg.solve(Lf.T if trans else Lf, B)
+    np.testing.assert_allclose(X, ref, rtol=1e-9, atol=1e-9 * np.abs(ref).max())
+    if nrhs == 1:
+        x1 = L.trsm(Lstore, B[:, 0], trans=trans).cpu().numpy()
+        np.testing.assert_allclose(x1, ref[:, 0], rtol=1e-9, atol=1e-9 * np.abs(ref).max())

@@ -73,6 +73,9 @@ SIGNATURES = {
     "vgposp_potrf_workspace_bytes": (_size, [_i64]),
     "vgposp_potrf_lower": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p,
                                   _c_void_p, _size, _c_void_p]),
+    "vgposp_trsm_workspace_bytes": (_size, [_i64, _i64]),
+    "vgposp_trsm_lower": (_i32, [_c_void_p, _i64, _i64, _i32, _c_void_p, _i64, _i64, _c_void_p,
+                                 _size, _c_void_p]),
     "vgposp_lml_workspace_bytes": (_size, [_i64, _i32]),
     "vgposp_lml": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
                           _c_void_p, _c_void_p, _size, _c_void_p]),

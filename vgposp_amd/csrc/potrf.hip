@@ -132,14 +132,20 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   __shared__ double XD[(NB / LW) * LW * LW];  // dense diagonal blocks of L^-1
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  // invert: 0 = factor (lower(A) <- L), 1 = factor and invert (lower(A) <- L^-1), 2 = A already
+  // holds L: only form L^-1 into linv (A is read, never written; the TRSM leaves).
+  const bool factor = invert != 2;
   A += blockIdx.x * stride_a;
   info += blockIdx.x;
+  if (linv) linv += (int64_t)blockIdx.x * NB * NB;
   if (diag_out) diag_out += (int64_t)blockIdx.x * jb;
   const int JP = (jb + LW - 1) & ~(LW - 1), NP = JP / LW;
   for (int e = t; e < NB * NB; e += LEAF_THREADS) {
     const int r = e / NB, c = e % NB;
     if (r < JP && c <= r) L[r * LP2 + c] = r < jb ? A[(int64_t)r * lda + c] : (r == c ? 1.0 : 0.0);
   }
+  if (!factor)
+    for (int c = t; c < JP; c += LEAF_THREADS) rdiag[c] = c < jb ? 1.0 / A[(int64_t)c * lda + c] : 1.0;
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
   long long ts = STAMP_NOW();
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   // Left-looking over 16-column panels:
   //   A[c0:, c0:c0+16] -= L[c0:, :c0] L[c0:c0+16, :c0]^T   (MFMA, 16-row tiles over the 4 waves)
   //   factor the tall panel A[c0:, c0:c0+16] in wave 0's registers (leaf_panel)
-  for (int p = 0; p < NP; ++p) {
+  for (int p = 0; factor && p < NP; ++p) {
     const int c0 = p * LW;
     if (p > 0) {
       const int nrt = NP - p;
@@ -274,7 +280,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
     double x = 0.0;
     if (r < jb && c <= r) x = (r == c) ? rdiag[c] : L[c * LP2 + r];
     if (linv) linv[e] = x;
-    if (r < jb && c <= r) A[(int64_t)r * lda + c] = invert ? x : L[r * LP2 + c];
+    if (factor && r < jb && c <= r) A[(int64_t)r * lda + c] = invert ? x : L[r * LP2 + c];
   }
   if (diag_out != nullptr) {
     for (int c = t; c < jb; c += LEAF_THREADS) diag_out[c] = L[c * LP2 + c];
@@ -443,14 +449,19 @@ size_t potrf_ws_bytes(int64_t n) {
   return (size_t)(leaves * NB * NB + n1 * (n - n1) + blk + part + 64) * sizeof(double);
 }
 
-int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
-              void* ws, hipStream_t stream) {
+static int ensure_leaf_attr() {
   static bool attr_set = false;
   if (!attr_set) {
     VG_HIP(hipFuncSetAttribute((const void*)potrf_leaf_kernel,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)leaf_shmem()));
     attr_set = true;
   }
+  return 0;
+}
+
+int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
+              void* ws, hipStream_t stream) {
+  if (int rc = ensure_leaf_attr()) return rc;
   const int64_t leaves = (n + NB - 1) / NB;
   const int64_t n1 = n > NB ? split_point(n) : 0;
   double* base = static_cast<double*>(ws);
@@ -465,7 +476,96 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
   return trtri_rec(f, A, lda, n, 0, blocks);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Left-side triangular solve with a factor from vgposp_potrf_lower(invert = 0):
+//   B (n x m) <- L^-1 B (trans = 0, forward)  or  L^-T B (trans = 1, backward)
+// Recursion on the same splits as potrf_rec: the off-diagonal part is one GEMM per level
+// (B2 -= L21 X1, or B1 -= L21^T X2), and the <= 128 diagonal blocks multiply by their inverses,
+// formed up front by the leaf kernel's invert-only mode (all full blocks in one launch).
+// ---------------------------------------------------------------------------------------------
+static int trsm_left_rec(const Fact& f, const double* Lp, int64_t ldl, int64_t n, int64_t col0,
+                         int trans, double* B, int64_t m, int64_t ldb) {
+  int rc;
+  if (n <= NB) {  // out of place (the n == 1 column path is a GEMV that may not alias), copy back
+    if ((rc = pgemm(f, trans, 0, n, m, n, 1.0, f.leaf(col0), NB, B, ldb, 0.0, f.tmp, m,
+                    VGPOSP_FULL, 0, 0)))
+      return rc;
+    VG_HIP(hipMemcpy2DAsync(B, ldb * sizeof(double), f.tmp, m * sizeof(double), m * sizeof(double),
+                            n, hipMemcpyDeviceToDevice, f.s));
+    return 0;
+  }
+  const int64_t a = split_point(n), b = n - a;
+  const double* L21 = Lp + a * ldl;
+  if (!trans) {
+    if ((rc = trsm_left_rec(f, Lp, ldl, a, col0, 0, B, m, ldb))) return rc;
+    if ((rc = pgemm(f, 0, 0, b, m, a, -1.0, L21, ldl, B, ldb, 1.0, B + a * ldb, ldb, VGPOSP_FULL,
+                    0, 0)))
+      return rc;
+    return trsm_left_rec(f, L21 + a, ldl, b, col0 + a, 0, B + a * ldb, m, ldb);
+  }
+  if ((rc = trsm_left_rec(f, L21 + a, ldl, b, col0 + a, 1, B + a * ldb, m, ldb))) return rc;
+  if ((rc = pgemm(f, 1, 0, a, m, b, -1.0, L21, ldl, B + a * ldb, ldb, 1.0, B, ldb, VGPOSP_FULL, 0,
+                  0)))
+    return rc;
+  return trsm_left_rec(f, Lp, ldl, a, col0, 1, B, m, ldb);
+}
+
+size_t trsm_ws_bytes(int64_t n, int64_t m) {
+  const int64_t leaves = (n + NB - 1) / NB;
+  return (size_t)(leaves * NB * NB + NB * m + PART_ELEMS + 64) * sizeof(double);
+}
+
+int trsm_left(const double* L, int64_t n, int64_t ldl, int trans, double* B, int64_t m,
+              int64_t ldb, void* ws, hipStream_t s) {
+  if (int rc = ensure_leaf_attr()) return rc;
+  double* leaves = static_cast<double*>(ws);
+  const int64_t nl = (n + NB - 1) / NB, nfull = n / NB;
+  double* tmp = leaves + nl * NB * NB;
+  double* part = tmp + NB * m;
+  int* dummy = reinterpret_cast<int*>(part + PART_ELEMS);  // the invert-only leaves never write it
+  {
+    ProfScope ps("trtri_leaf", s, 0.0, 8.0 * NB * NB * 2 * nl);
+    if (nfull > 0)
+      hipLaunchKernelGGL(potrf_leaf_kernel, dim3((unsigned)nfull), dim3(LEAF_THREADS), leaf_shmem(),
+                         s, const_cast<double*>(L), ldl, NB, (int64_t)0, 2, leaves,
+                         (double*)nullptr, dummy, (int64_t)NB * (ldl + 1));
+    if (nl > nfull)
+      hipLaunchKernelGGL(potrf_leaf_kernel, dim3(1), dim3(LEAF_THREADS), leaf_shmem(), s,
+                         const_cast<double*>(L) + nfull * NB * (ldl + 1), ldl, (int)(n - nfull * NB),
+                         (int64_t)0, 2, leaves + nfull * NB * NB, (double*)nullptr, dummy,
+                         (int64_t)0);
+    VG_LAUNCH_CHECK();
+  }
+  Fact f{ldl, leaves, nullptr, nullptr, tmp, nullptr, dummy, part, s};
+  return trsm_left_rec(f, L, ldl, n, 0, trans, B, m, ldb);
+}
+
 }  // namespace vgposp
+
+extern "C" size_t vgposp_trsm_workspace_bytes(int64_t n, int64_t nrhs) {
+  return n > 0 && nrhs > 0 ? vgposp::trsm_ws_bytes(n, nrhs) : 0;
+}
+
+extern "C" int vgposp_trsm_lower(const double* L, int64_t n, int64_t ldl, int trans, double* B,
+                                 int64_t nrhs, int64_t ldb, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(L != nullptr || n == 0, 1);
+  VG_CHECK_ARG(n >= 0, 2);
+  VG_CHECK_ARG(ldl >= (n > 0 ? n : 1), 3);
+  VG_CHECK_ARG(trans == 0 || trans == 1, 4);
+  VG_CHECK_ARG(B != nullptr || n == 0 || nrhs == 0, 5);
+  VG_CHECK_ARG(nrhs >= 0, 6);
+  VG_CHECK_ARG(ldb >= (nrhs > 0 ? nrhs : 1), 7);
+  VG_CHECK_ARG(ws != nullptr || n == 0, 8);
+  if (n == 0 || nrhs == 0) return 0;
+  if (ws_bytes < trsm_ws_bytes(n, nrhs)) {
+    set_error("vgposp_trsm_lower: workspace %zu < %zu bytes", ws_bytes, trsm_ws_bytes(n, nrhs));
+    return VGPOSP_E_WS;
+  }
+  return trsm_left(L, n, ldl, trans, B, nrhs, ldb, ws, as_stream(stream));
+}
 
 extern "C" size_t vgposp_potrf_workspace_bytes(int64_t n) {
   return n > 0 ? vgposp::potrf_ws_bytes(n) : 0;

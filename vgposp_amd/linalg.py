@@ -167,6 +167,24 @@ def cholesky(A):
     return torch.tril(L)
 
 
+def trsm(L, B, trans=False):
+    """X = L^-1 B (trans=False) or L^-T B (trans=True) for a lower factor L [n, n] (upper triangle
+    ignored) and B [n] or [n, m]; returns a new device tensor (tf.linalg.triangular_solve)."""
+    L = as_device(L)
+    X = as_device(B).clone()
+    vec = X.dim() == 1
+    X2 = X.reshape(-1, 1) if vec else X
+    n = L.shape[-1]
+    if L.dim() != 2 or L.shape[0] != n or X2.shape[0] != n:
+        raise ValueError(f"trsm: L {tuple(L.shape)} and B {tuple(X.shape)} do not conform")
+    if not L.is_contiguous():
+        L = L.contiguous()
+    ws = workspace(query("vgposp_trsm_workspace_bytes", n, X2.shape[1]))
+    call("vgposp_trsm_lower", _p(L), n, L.stride(0), int(bool(trans)), _p(X2), X2.shape[1],
+         X2.stride(0), _p(ws), ws.numel(), _stream())
+    return X
+
+
 def tri_inverse_from_factor(Minv):
     """Lower-triangular part of an in-place inverted factor."""
     return torch.tril(Minv)

@@ -2,6 +2,8 @@
 
 * ``placement_split``: one 64 x 32 x 32 split (N = 65,536) of the greedy benchmark: a jittered
   grid (seed = rank, shifted along axis 0 by rank), EQ kernel, amp 1, ls = 2h, noise 1e-2 + 1e-6.
+* ``c2_data``: config C2, the 32^3 grid for K assembly + potrf.
+* ``vgp_c5_data``: config C5, 5-D uniform observations with a 4^5 inducing grid (M = 1,024).
 * ``vgp_c3``: config C3.  N = 64^3 observations on a grid over [-7, 7]^3, M = 8^3 inducing points
   on the sub-grid (spacing 2, twice the initial length scale, so the unjittered Kzz whose log-det
   the KL term needs stays well conditioned).  Target y = sum_d exp(-x_d^2 / 20) sin(x_d) +
@@ -31,6 +33,26 @@ def vgp_c3_data(n=64, m=8, half=7.0, seed=0):
     gz = np.linspace(-half, half, m)
     Z = np.stack(np.meshgrid(gz, gz, gz, indexing="ij"), -1).reshape(-1, 3)
     return X, y, Z
+
+
+def vgp_c5_data(n=65536, m=4, d=5, half=2.0, seed=0):
+    """Config C5: X ~ U[-2, 2]^5 (N = 65,536), M = 4^5 = 1,024 inducing points on a grid (spacing
+    4/3 > the initial length scale, so the unjittered Kzz stays well conditioned), the d-dim form
+    of the C3 target."""
+    rng = np.random.default_rng(seed)
+    X = rng.uniform(-half, half, (n, d))
+    y = np.sum(np.exp(-X ** 2 / 20.0) * np.sin(X), axis=1) + rng.normal(0, 0.1, n)
+    gz = np.linspace(-half, half, m)
+    Z = np.stack(np.meshgrid(*([gz] * d), indexing="ij"), -1).reshape(-1, d)
+    return X, y, Z
+
+
+def c2_data(n=32, half=2.0):
+    """Config C2: a 32^3 grid over linspace(-2, 2) per axis (N = 32,768), EQ amp 1, ls = 2h,
+    noise 1e-2 + 1e-6."""
+    shape = (n, n, n)
+    X = grid_points(shape)
+    return X, 2.0 * grid_spacing(shape)
 
 
 def vgp_c3_graph(X, y, Z, B, lr=0.01):
