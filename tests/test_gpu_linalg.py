@@ -175,3 +175,30 @@ def test_trsm(L, n, nrhs, trans):
     if nrhs == 1:
         x1 = L.trsm(Lstore, B[:, 0], trans=trans).cpu().numpy()
         np.testing.assert_allclose(x1, ref[:, 0], rtol=1e-9, atol=1e-9 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("ta", [0, 1])
+@pytest.mark.parametrize("tb", [0, 1])
+@pytest.mark.parametrize("tri_a", [0, 1])
+@pytest.mark.parametrize("tri_b", [0, 1])
+@pytest.mark.parametrize("shape", ["square", "vector"])
+def test_gemm_all_flags(L, ta, tb, tri_a, tri_b, shape):
+    """Every (transa, transb, tri_a, tri_b) combination on the fast kernel, and the triangular
+    mat-vec paths (n == 1): a stored triangular operand has garbage above its diagonal."""
+    if shape == "vector" and (tri_b or tb):
+        pytest.skip("a column vector B is neither transposed nor triangular here")
+    m = k = 320
+    n = 1 if shape == "vector" else (k if tri_b else 256)
+    rng = np.random.default_rng(ta + 2 * tb + 4 * tri_a + 8 * tri_b + (16 if n == 1 else 0))
+    As = rng.standard_normal((k, m) if ta else (m, k))
+    Bs = rng.standard_normal((n, k) if tb else (k, n))
+    Ae = np.tril(As) if tri_a else As
+    Be = np.tril(Bs) if tri_b else Bs
+    opA = Ae.T if ta else Ae
+    opB = Be.T if tb else Be
+    C0 = rng.standard_normal((m, n))
+    C = L.as_device(C0.copy())
+    L.gemm(As, Bs, C, alpha=1.25, beta=-0.5, transa=bool(ta), transb=bool(tb), tri_a=bool(tri_a),
+           tri_b=bool(tri_b))
+    np.testing.assert_allclose(C.cpu().numpy(), 1.25 * opA @ opB - 0.5 * C0, rtol=1e-11,
+                               atol=1e-11)

@@ -42,6 +42,7 @@ struct GemmParams {
   int nsplit, nblk;
   int64_t kchunk;
   double* part;
+  int prio;  // experiment (VGPOSP_GEMM_PRIO): 1 = s_setprio 1 for the second wave of each SIMD pair
 };
 
 // Stage one operand tile (128 rows of the M/N dimension x 16 of K) into registers.
@@ -274,22 +275,32 @@ __device__ __forceinline__ int tri_root(int64_t id) {
   return (int)t;
 }
 
-// BMW = 128-row A sub-tiles per workgroup, always 4 waves in a 2x2 grid:
-//   1 -> 128x128 tiles, 64x64 per wave (4x4 fragments), STAGES-deep ring, 2 workgroups per CU;
-//   2 -> 256x128 tiles, 128x64 per wave (8x4 fragments, 128 accumulators in AGPRs), 3-stage ring
-//        (144 KiB), 1 workgroup per CU: a third fewer LDS fragment reads and operand bytes per
-//        MFMA, latency hidden by the deeper ring instead of a second workgroup.
-template <bool TA, bool TB, bool TRIA, bool TRIB, int BMW>
-__global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds_kernel(
+// CFG selects the tile shape (waves always in a (rows / 64 or 128) x 2 grid over the tile):
+//   1 -> 128x128 tiles, 4 waves of 64x64 (4x4 fragments), STAGES-deep ring, 2 workgroups per CU;
+//   2 -> 256x128 tiles, 4 waves of 128x64 (8x4 fragments, 128 accumulators in AGPRs), 3-stage
+//        ring (144 KiB), 1 workgroup per CU;
+//   3 -> 256x128 tiles, 8 waves of 64x64, 3-stage ring, 1 workgroup per CU: two waves per SIMD
+//        as in 1, but 6 instead of 8 LDS-DMA pieces per wave per 64 MFMAs and a deeper ring.
+template <int CFG> struct GemmCfg {
+  static constexpr int NSUB = CFG == 1 ? 1 : 2;              // 128-row A sub-tiles
+  static constexpr int NW = CFG == 3 ? 8 : 4;                // waves
+  static constexpr int FI = CFG == 2 ? 8 : 4;                // 16-row fragments per wave
+  static constexpr int NST = CFG == 1 ? STAGES : 3;          // ring depth
+  static constexpr int OCC = CFG == 1 ? VGPOSP_GEMM_OCC : 1;  // workgroups per CU (launch bound)
+};
+
+template <bool TA, bool TB, bool TRIA, bool TRIB, int CFG>
+__global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm_glds_kernel(
     GemmParams p, int tiles_m, int tiles_n) {
   constexpr bool A_KC = !TA;
   constexpr bool B_KC = TB;
-  constexpr int TBM = GBM * BMW;                       // rows per tile
-  constexpr int WROWS = 64 * BMW;                      // rows per wave
-  constexpr int FI = 4 * BMW;                          // 16-row fragments per wave
-  constexpr int NST = BMW == 1 ? STAGES : 3;           // ring depth
-  constexpr int SE = (BMW + 1) * OPND_ELEMS;           // doubles per stage: A subs | B
-  constexpr int PPW = 4 * (BMW + 1);                   // pieces per wave per stage (8 or 12)
+  constexpr int NSUB = GemmCfg<CFG>::NSUB, NW = GemmCfg<CFG>::NW, FI = GemmCfg<CFG>::FI;
+  constexpr int NST = GemmCfg<CFG>::NST;
+  constexpr int TBM = GBM * NSUB;                      // rows per tile
+  constexpr int WROWS = 16 * FI;                       // rows per wave
+  constexpr int SE = (NSUB + 1) * OPND_ELEMS;          // doubles per stage: A subs | B
+  constexpr int PO = 16 / NW;                          // pieces per operand per wave
+  constexpr int PPW = PO * (NSUB + 1);                 // pieces per wave per stage (8, 12 or 6)
   constexpr bool SPREAD = NST >= 3;                    // next-tile loads between the MFMAs
   __shared__ double smem[NST * SE];
 
@@ -328,6 +339,7 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fk = lane >> 4;
+  if (p.prio == 1 && (NW == 8 ? wave >= 4 : (bid >> 3) & 1)) __builtin_amdgcn_s_setprio(1);
 
   // K range that can contribute when an operand is stored lower triangular.
   int64_t kbeg = 0, kend = p.k;
@@ -354,19 +366,17 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
 
-  // stage layout: [A sub-tile 0 | ... | A sub-tile BMW-1 | B].  Every wave issues 4 pieces of each
-  // A sub-tile and 4 of B, with no branches (measured: splitting the waves into A-loaders and
-  // B-loaders cost 10% on 8192^3).
-  // piece q (0 .. PPW-1) of this wave for K-tile t: q / 4 = operand (A sub-tiles, then B)
+  // stage layout: [A sub-tile 0 | ... | A sub-tile NSUB-1 | B].  Every wave issues PO pieces of
+  // each operand, with no branches (measured: splitting the waves into A-loaders and B-loaders
+  // cost 10% on 8192^3).  Piece q (0 .. PPW-1) of this wave for K-tile t: q / PO = operand.
   auto issue_piece = [&](int t, int q) {
     double* st = smem + (t % NST) * SE;
     const int64_t k0 = kbeg + (int64_t)t * GBK;
-    const int op = q >> 2, j = q & 3;
-    if (op < BMW)
-      glds_piece<A_KC>(p.A, p.lda, m0 + GBM * op, k0, p.m, p.k, st + op * OPND_ELEMS, wave * 4 + j,
-                       lane);
+    const int op = q / PO, j = wave * PO + q % PO;
+    if (op < NSUB)
+      glds_piece<A_KC>(p.A, p.lda, m0 + GBM * op, k0, p.m, p.k, st + op * OPND_ELEMS, j, lane);
     else
-      glds_piece<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + BMW * OPND_ELEMS, wave * 4 + j, lane);
+      glds_piece<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + NSUB * OPND_ELEMS, j, lane);
   };
   auto issue = [&](int t) {
 #pragma unroll
@@ -379,15 +389,18 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
 
   for (int t = 0; t < T; ++t) {
     const int after = min(T - 1 - t, NST - 2);  // tiles that may stay in flight
-    static_assert(PPW == 8 || PPW == 12, "counted waits below assume 8 or 12 pieces per wave");
-    if (PPW == 8) {
+    static_assert(PPW == 8 || PPW == 12 || PPW == 6, "counted waits: 6, 8 or 12 pieces");
+    if (after == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (PPW == 8) {
       if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (PPW == 12) {
       if (after >= 2) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -397,8 +410,8 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
     const bool more = t + NST - 1 < T;
     if (!SPREAD && more) issue(t + NST - 1);
 
-    const double* As = smem + (t % NST) * SE + (BMW == 1 ? 0 : wm * OPND_ELEMS);
-    const double* Bs = smem + (t % NST) * SE + BMW * OPND_ELEMS;
+    const double* As = smem + (t % NST) * SE + ((wm * WROWS) / GBM) * OPND_ELEMS;
+    const double* Bs = smem + (t % NST) * SE + NSUB * OPND_ELEMS;
     const int64_t k0 = kbeg + (int64_t)t * GBK;
     // masks only where needed: the last partial K-tile, and K-tiles that straddle the diagonal
     // of a triangular operand (k0 within 128 of the tile's first row / column)
@@ -410,7 +423,7 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
       double a[FI], b[4];
 #pragma unroll
       for (int i = 0; i < FI; ++i) {
-        const int r = (BMW == 1 ? wm * 64 : 0) + i * 16 + fr;  // row within the sub-tile
+        const int r = (wm * WROWS) % GBM + i * 16 + fr;  // row within the sub-tile
         a[i] = As[frag_off<A_KC>(r, k)];
       }
 #pragma unroll
@@ -433,7 +446,7 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
       }
       if (SPREAD && more) {
 #pragma unroll
-        for (int q = ks * (PPW / 4); q < (ks + 1) * (PPW / 4); ++q) issue_piece(t + NST - 1, q);
+        for (int q = (ks * PPW) / 4; q < ((ks + 1) * PPW) / 4; ++q) issue_piece(t + NST - 1, q);
       }
 #pragma unroll
       for (int i = 0; i < FI; ++i)
@@ -467,18 +480,30 @@ __global__ __launch_bounds__(256, BMW == 1 ? VGPOSP_GEMM_OCC : 1) void gemm_glds
   }
 }
 
-template <int BMW>
+template <int CFG, bool TA, bool TB, bool TRIA, bool TRIB>
+static void launch_one(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn) {
+  hipLaunchKernelGGL((gemm_glds_kernel<TA, TB, TRIA, TRIB, CFG>), g1, dim3(64 * GemmCfg<CFG>::NW),
+                     0, stream, p, tm, tn);
+}
+
+// every (transa, transb, tri_a, tri_b) combination: the kernel's K-range and mask logic is
+// generic in the four flags.  The 256x128 configurations are instantiated for plain operands only.
+template <int CFG, bool TA, bool TB>
+static void launch_tri(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn, int tri_a,
+                       int tri_b) {
+  if (CFG != 1 || (!tri_a && !tri_b)) return launch_one<CFG, TA, TB, false, false>(g1, stream, p, tm, tn);
+  if (tri_a && tri_b) return launch_one<1, TA, TB, true, true>(g1, stream, p, tm, tn);
+  if (tri_a) return launch_one<1, TA, TB, true, false>(g1, stream, p, tm, tn);
+  launch_one<1, TA, TB, false, true>(g1, stream, p, tm, tn);
+}
+
+template <int CFG>
 static void launch_glds(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn,
                         int transa, int transb, int tri_a, int tri_b) {
-  const dim3 blk(256);
-  if (tri_a && tri_b) hipLaunchKernelGGL((gemm_glds_kernel<true, false, true, true, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else if (tri_b && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, true, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else if (tri_a) hipLaunchKernelGGL((gemm_glds_kernel<false, false, true, false, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else if (tri_b) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, true, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else if (!transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<false, false, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else if (!transa && transb) hipLaunchKernelGGL((gemm_glds_kernel<false, true, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else if (transa && !transb) hipLaunchKernelGGL((gemm_glds_kernel<true, false, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
-  else hipLaunchKernelGGL((gemm_glds_kernel<true, true, false, false, BMW>), g1, blk, 0, stream, p, tm, tn);
+  if (!transa && !transb) launch_tri<CFG, false, false>(g1, stream, p, tm, tn, tri_a, tri_b);
+  else if (!transa) launch_tri<CFG, false, true>(g1, stream, p, tm, tn, tri_a, tri_b);
+  else if (!transb) launch_tri<CFG, true, false>(g1, stream, p, tm, tn, tri_a, tri_b);
+  else launch_tri<CFG, true, true>(g1, stream, p, tm, tn, tri_a, tri_b);
 }
 
 // C = sum_z part[z] + beta * C over the (lower) output, fixed summation order.
@@ -502,10 +527,11 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int64_t m, int6
 __global__ __launch_bounds__(256) void gemv_rows_kernel(int64_t m, int64_t k, double alpha,
                                                         const double* A, int64_t lda,
                                                         const double* x, int64_t incx, double beta,
-                                                        double* y, int64_t incy) {
+                                                        double* y, int64_t incy, int tri) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= m) return;
+  if (tri) k = min(k, r + 1);  // stored lower triangular: A[r][c] = 0 for c > r
   const double* row = A + r * lda;
   double s0 = 0.0, s1 = 0.0;
   int64_t c = lane;
@@ -527,11 +553,11 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(int64_t m, int64_t k, do
 __global__ __launch_bounds__(256) void gemv_rows_split_kernel(int64_t m, int64_t k, int64_t kchunk,
                                                               const double* A, int64_t lda,
                                                               const double* x, int64_t incx,
-                                                              double* part) {
+                                                              double* part, int tri) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= m) return;
-  const int64_t k0 = (int64_t)blockIdx.y * kchunk, k1 = min(k, k0 + kchunk);
+  const int64_t k0 = (int64_t)blockIdx.y * kchunk, k1 = min(tri ? min(k, r + 1) : k, k0 + kchunk);
   const double* row = A + r * lda;
   double s0 = 0.0, s1 = 0.0;
   int64_t c = k0 + lane;
@@ -549,10 +575,13 @@ __global__ __launch_bounds__(256) void gemv_rows_split_kernel(int64_t m, int64_t
 __global__ __launch_bounds__(256) void gemv_t_kernel(int64_t m, int64_t k, int64_t kchunk,
                                                      double alpha, const double* A, int64_t lda,
                                                      const double* x, int64_t incx, double beta,
-                                                     double* y, int64_t incy, double* part) {
+                                                     double* y, int64_t incy, double* part,
+                                                     int tri) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= m) return;
-  const int64_t k0 = (int64_t)blockIdx.y * kchunk, k1 = min(k, k0 + kchunk);
+  // tri: A stored k x m lower triangular, A[c][j] = 0 for j > c, so only c >= j contribute
+  const int64_t k0 = max((int64_t)blockIdx.y * kchunk, tri ? j : (int64_t)0);
+  const int64_t k1 = min(k, (int64_t)blockIdx.y * kchunk + kchunk);
   double s0 = 0.0, s1 = 0.0;
   int64_t c = k0;
   for (; c + 1 < k1; c += 2) {
@@ -589,13 +618,19 @@ static int gemv_splits(int64_t m, int64_t k, int transa) {
   return (int)std::max<int64_t>(std::min<int64_t>(s, 4096), 1);
 }
 
-int g_fast_gemm = 1;  // 0 forces the reference kernel (tests)
-// 256x128 tiles (BMW = 2) only on request (VGPOSP_GEMM_BMW=2): measured on one box, 8192^3 NT
-// 68.0 vs 68.9 TF/s and the 65k Cholesky + inverse 3.23 vs 3.18 s against 128x128 at two
-// workgroups per CU — the fewer bytes per flop do not pay once two waves share each SIMD.
-static const bool g_bmw2 = [] {
-  const char* e = getenv("VGPOSP_GEMM_BMW");
-  return e && e[0] == '2';
+int g_fast_gemm = [] {  // 0 forces the register-staged reference kernel (VGPOSP_GEMM_REF=1)
+  const char* e = getenv("VGPOSP_GEMM_REF");
+  return e && e[0] == '1' ? 0 : 1;
+}();
+// 256x128 configurations (gemm_glds_kernel CFG 2 / 3) only on request, VGPOSP_GEMM_CFG=2 or 3,
+// for full-C launches with at least two rounds of workgroups (measurements in DESIGN.md §4).
+static const int g_prio = [] {
+  const char* e = getenv("VGPOSP_GEMM_PRIO");
+  return e ? atoi(e) : 0;
+}();
+static const int g_cfg = [] {
+  const char* e = getenv("VGPOSP_GEMM_CFG");
+  return (e && (e[0] == '2' || e[0] == '3')) ? e[0] - '0' : 1;
 }();
 
 static bool aligned16(const void* ptr, int64_t ld) {
@@ -607,7 +642,7 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
                       double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
                       double* part, hipStream_t stream) {
   if (m <= 0 || n <= 0) return 0;
-  if (n == 1 && !tri_a && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
+  if (n == 1 && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
     ProfScope ps("gemv_f64", stream, 2.0 * (double)m * k, 8.0 * ((double)m * k + k + 2.0 * m));
     const int64_t incx = transb ? 1 : ldb;
     const int S = (nsplit > 1 && part != nullptr) ? nsplit : 1;
@@ -615,15 +650,15 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     if (!transa) {
       if (S == 1) {
         hipLaunchKernelGGL(gemv_rows_kernel, dim3((unsigned)ceil_div(m, 4)), dim3(256), 0, stream, m,
-                           k, alpha, A, lda, B, incx, beta, C, ldc);
+                           k, alpha, A, lda, B, incx, beta, C, ldc, tri_a);
       } else {
         hipLaunchKernelGGL(gemv_rows_split_kernel, dim3((unsigned)ceil_div(m, 4), (unsigned)S),
-                           dim3(256), 0, stream, m, k, kchunk, A, lda, B, incx, part);
+                           dim3(256), 0, stream, m, k, kchunk, A, lda, B, incx, part, tri_a);
       }
     } else {
       hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)ceil_div(m, 256), (unsigned)S), dim3(256), 0,
                          stream, m, k, kchunk, alpha, A, lda, B, incx, beta, C, ldc,
-                         S > 1 ? part : nullptr);
+                         S > 1 ? part : nullptr, tri_a);
     }
     VG_LAUNCH_CHECK();
     if (S > 1) {
@@ -633,16 +668,15 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     }
     return 0;
   }
-  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr};
+  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr,
+               g_prio};
   const int va = aligned16(A, lda), vb = aligned16(B, ldb);
   const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
-  const bool tri_ok = (!tri_a && !tri_b) || (!transa && !transb && (tri_a != tri_b)) ||
-                      (!transa && transb && !tri_a && tri_b) || (transa && !transb && tri_a && tri_b);
-  if (va && vb && even && tri_ok && g_fast_gemm) {
-    // 256x128 tiles (8 waves) for full-C launches with at least two rounds of workgroups, on request
-    const int bmw = (uplo_c == VGPOSP_FULL && g_bmw2 &&
-                     ceil_div(m, 2 * GBM) * ceil_div(n, GBN) >= 512) ? 2 : 1;
-    const int tm = (int)ceil_div(m, GBM * bmw), tn = (int)ceil_div(n, GBN);
+  if (va && vb && even && g_fast_gemm) {
+    // 256x128 tiles for full-C launches with at least two rounds of workgroups, on request
+    const int cfg = (uplo_c == VGPOSP_FULL && g_cfg > 1 && !tri_a && !tri_b &&
+                     ceil_div(m, 2 * GBM) * ceil_div(n, GBN) >= 512) ? g_cfg : 1;
+    const int tm = (int)ceil_div(m, GBM * (cfg == 1 ? 1 : 2)), tn = (int)ceil_div(n, GBN);
     const int64_t nblk = (uplo_c == VGPOSP_LOWER) ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
     const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
     // algorithmic flops: a triangular operand halves the useful products
@@ -664,7 +698,8 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
                uplo_c == VGPOSP_LOWER ? 'L' : 'F', tri_a ? 'a' : '-', tri_b ? 'b' : '-', p.nsplit);
     ProfScope pshape(shape_name, stream, fl, 0.0, shapes && prof_on());
     dim3 g1((unsigned)(nblk * p.nsplit));
-    if (bmw == 2) launch_glds<2>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    if (cfg == 2) launch_glds<2>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    else if (cfg == 3) launch_glds<3>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     else launch_glds<1>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     VG_LAUNCH_CHECK();
     if (p.nsplit > 1) {

@@ -109,8 +109,8 @@ def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=
     n = B.shape[0] if transb else B.shape[1]
     if k != kb:
         raise ValueError(f"inner dimensions differ: {k} vs {kb}")
-    if C is None:
-        C = torch.zeros((m, n), dtype=F64, device=A.device)
+    if C is None:  # a lower-C result keeps a zero upper triangle; a full one is written entirely
+        C = (torch.zeros if lower_c else torch.empty)((m, n), dtype=F64, device=A.device)
         beta = 0.0
     uplo = LOWER if lower_c else FULL
     if splitk:
