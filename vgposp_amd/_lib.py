@@ -163,8 +163,17 @@ def query(name, *args):
     return int(getattr(load(), name)(*args))
 
 
+_prof_state = [False]
+
+
 def prof_enable(on=True):
     call("vgposp_prof_enable", int(on))
+    _prof_state[0] = bool(on)
+
+
+def prof_on():
+    """Whether the library's per-launch event timing is on (set through prof_enable)."""
+    return _prof_state[0]
 
 
 def prof_query(name):

@@ -181,8 +181,11 @@ class VGPObjective:
             st.update(fac[0])
         return st
 
-    def loss_and_grads(self, Z, amp, ls, noise, Xb, yb, kl_weight, want_grads=True):
-        """-> (loss, d/damp, d/dls, d/dnoise, d/dZ [M, d]) as 0-d / [M, d] device tensors."""
+    def loss_and_grads(self, Z, amp, ls, noise, Xb, yb, kl_weight, want_grads=True, infos=None):
+        """-> (loss, d/damp, d/dls, d/dnoise, d/dZ [M, d]) as 0-d / [M, d] device tensors.
+
+        No host synchronisation unless ``infos`` is None: with a list, the device Cholesky
+        statuses are appended for the caller to check (the graph-captured training step)."""
         Z = linalg.as_device(Z)
         Z = Z[:, None] if Z.dim() == 1 else Z
         Xb = linalg.as_device(Xb)
@@ -191,8 +194,10 @@ class VGPObjective:
         a, l, s = (linalg.as_device(v).reshape(()) for v in (amp, ls, noise))
         j, w = self.j, float(kl_weight)
         M, nb = Z.shape[0], yb.numel()
-        s_h = float(s)  # host copy for GEMM alphas (the one sync of a step)
-        infos = []      # Cholesky statuses, checked once at the end
+        check = infos is None
+        infos = [] if check else infos  # Cholesky statuses, checked once at the end
+        # every 1 / s factor is applied on device to an M x M operand (no host copy of s)
+        s_inv = 1.0 / s
         st = self._forward_posterior(Z, a, l, s, infos, side=True)
         Kzz, Kzx, P0, c, Li, logdetL, t, m, A = (st[k] for k in
                                                  ("Kzz", "Kzx", "P0", "c", "Li", "logdetL", "t",
@@ -217,8 +222,9 @@ class VGPObjective:
         KL = logdetLp - logdetA + 0.5 * (-M + torch.sum(PA * PA) + torch.sum(qm * qm))
         E = obs - T - w * KL
         if not want_grads:
-            for info in infos:
-                linalg.check_info(info)
+            if check:
+                for info in infos:
+                    linalg.check_info(info)
             return -E, None, None, None, None
         # ---- reverse pass (d E) ----
         mu_b = r / s2
@@ -228,13 +234,14 @@ class VGPObjective:
         Kzz_b = -torch.outer(u, v)
         s_b = s_b + T / s
         a_b = -nb * a / s
-        linalg.gemm(H, H, Kzz_b, alpha=-0.5 / s_h, beta=1.0, transb=True)
+        Kzz_b -= (0.5 * s_inv) * linalg.gemm(H, H, transb=True)
+        A_ms = A * (-s_inv)
         if self.trace_adjoint:
-            A_b = linalg.gemm(H, R, transb=True, alpha=-1.0 / s_h)
-            H_b = linalg.gemm(A, R, alpha=-1.0 / s_h)
+            A_b = linalg.gemm(H, R, transb=True) * (-s_inv)
+            H_b = linalg.gemm(A_ms, R)
         else:
-            A_b = linalg.gemm(R, H, transb=True, alpha=-1.0 / s_h)
-            H_b = linalg.gemm(A, R, transa=True, alpha=-1.0 / s_h)
+            A_b = linalg.gemm(R, H, transb=True) * (-s_inv)
+            H_b = linalg.gemm(A_ms, R, transa=True)
         Kzb_b = H / s
         KH = linalg.gemm(Kzj_inv, H_b)
         Kzb_b += KH
@@ -265,7 +272,7 @@ class VGPObjective:
         Kzz_b += Sinv_b
         s_b = s_b - torch.sum(Sinv_b * P0) / (s * s)
         # Kzx_bar = (2 / s) Sinv_b Kzx + c_b y^T  (rank-1 term fused into the VJP)
-        Kzx_b = linalg.gemm(Sinv_b, Kzx, alpha=2.0 / s_h)
+        Kzx_b = linalg.gemm(Sinv_b * (2.0 * s_inv), Kzx)
         g2, Zb2 = kernel_vjp(self.kind, Z, self.X, a, l, Kzx_b, c_b, self.y)
         red = torch.cat([g2, Zb2.reshape(-1)])
         self._allreduce(red)
@@ -275,8 +282,9 @@ class VGPObjective:
         a_b = a_b + 0.5 * g1[0] + g2[0] + g3[0]
         l_b = 0.5 * g1[1] + g2[1] + g3[1]
         Z_b = Zb1 + Zb2 + Zb3
-        for info in infos:
-            linalg.check_info(info)
+        if check:
+            for info in infos:
+                linalg.check_info(info)
         return -E, -a_b, -l_b, -s_b, -Z_b
 
 
