@@ -212,10 +212,13 @@ class VGPObjective:
         s2 = s + j
         rr = torch.dot(r, r)
         obs = -0.5 * rr / s2 - 0.5 * nb * torch.log(2.0 * math.pi * s2)
-        G = linalg.gemm(Lzi, Kzb, tri_a=True)
+        # Trace term with two M x B products instead of three: with H = Kzj^-1 Kzb (Kzj^-1 =
+        # Lzi^T Lzi) and R = op(A) H,  tr(G^T G) = <Kzb, H> for G = Lzi Kzb, and
+        # tr(R^T R) = <Q, H H^T> with Q = A^T A (A A^T for the trace_adjoint form).
         H = linalg.gemm(Kzj_inv, Kzb)
-        R = linalg.gemm(A, H, transa=self.trace_adjoint)
-        T = 0.5 * (nb * a * a - torch.sum(G * G) + torch.sum(R * R)) / s
+        HHt = _sym_from_lower(linalg.gemm(H, H, transb=True, lower_c=True))
+        Q = linalg.gemm(A, A, transa=not self.trace_adjoint, transb=self.trace_adjoint)
+        T = 0.5 * (nb * a * a - torch.dot(Kzb.reshape(-1), H.reshape(-1)) + torch.sum(Q * HHt)) / s
         logdetA = 2.0 * logdetLk - logdetL
         PA = linalg.gemm(Lpi, A, tri_a=True)
         qm = linalg.gemm(Lpi, _col(m), tri_a=True)
@@ -234,18 +237,17 @@ class VGPObjective:
         Kzz_b = -torch.outer(u, v)
         s_b = s_b + T / s
         a_b = -nb * a / s
-        Kzz_b -= (0.5 * s_inv) * linalg.gemm(H, H, transb=True)
-        A_ms = A * (-s_inv)
-        if self.trace_adjoint:
-            A_b = linalg.gemm(H, R, transb=True) * (-s_inv)
-            H_b = linalg.gemm(A_ms, R)
-        else:
-            A_b = linalg.gemm(R, H, transb=True) * (-s_inv)
-            H_b = linalg.gemm(A_ms, R, transa=True)
-        Kzb_b = H / s
-        KH = linalg.gemm(Kzj_inv, H_b)
-        Kzb_b += KH
-        linalg.gemm(KH, H, Kzz_b, alpha=-1.0, beta=1.0, transb=True)
+        Kzz_b -= (0.5 * s_inv) * HHt
+        # dE/dR = -R / s gives A_b = -(1/s) R H^T = -(1/s) A HHt (HHt A for trace_adjoint) and
+        # H_b = -(1/s) Q H; through H = Kzj^-1 Kzb: Kzb_b += Kzj^-1 H_b, Kzz_b -= Kzj^-1 H_b H^T.
+        # With P = Kzj^-1 Q all of it is M x M work plus one M x B product:
+        #   Kzb_b = H / s + Kzj^-1 H_b = ((I - P) / s) H,   Kzz_b += (1/s) P HHt.
+        A_b = (linalg.gemm(HHt, A) if self.trace_adjoint else linalg.gemm(A, HHt)) * (-s_inv)
+        P = linalg.gemm(Kzj_inv, Q)
+        Kzz_b += s_inv * linalg.gemm(P, HHt)
+        W = -P
+        W.diagonal().add_(1.0)
+        Kzb_b = linalg.gemm(W * s_inv, H)
         QA = linalg.gemm(Kp_inv, A)
         qv = linalg.gemm(Kp_inv, _col(m)).reshape(-1)
         A_b -= w * QA
