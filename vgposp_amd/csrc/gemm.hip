@@ -390,7 +390,11 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   for (int t = 0; t < T; ++t) {
     const int after = min(T - 1 - t, NST - 2);  // tiles that may stay in flight
     static_assert(PPW == 8 || PPW == 12 || PPW == 6, "counted waits: 6, 8 or 12 pieces");
+#ifdef VGPOSP_GEMM_EXP_NOVMWAIT  // timing experiment only: results are wrong
+    if (false) {
+#else
     if (after == 0) {
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (PPW == 8) {
       if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -403,11 +407,17 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
       else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef VGPOSP_GEMM_EXP_NOBARRIER  // timing experiment only: results are wrong
     __builtin_amdgcn_s_barrier();
+#endif
     // 3-stage ring: the next K-tile's pieces are spread over the k-slices below, between MFMAs
     // (issued back to back they park the wave for their issue cost; 8192^3 NT 63.3 -> 65.7 TF/s).
     // 2-stage ring: issued here, as early as possible — the tile is needed one K-step later.
+#ifdef VGPOSP_GEMM_EXP_NOLOADS  // timing experiment only: no loads after the prologue
+    const bool more = false;
+#else
     const bool more = t + NST - 1 < T;
+#endif
     if (!SPREAD && more) issue(t + NST - 1);
 
     const double* As = smem + (t % NST) * SE + ((wm * WROWS) / GBM) * OPND_ELEMS;
