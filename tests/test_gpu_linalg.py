@@ -202,3 +202,36 @@ def test_gemm_all_flags(L, ta, tb, tri_a, tri_b, shape):
            tri_b=bool(tri_b))
     np.testing.assert_allclose(C.cpu().numpy(), 1.25 * opA @ opB - 0.5 * C0, rtol=1e-11,
                                atol=1e-11)
+
+
+@pytest.mark.parametrize("ta,tb,tri_a,tri_b", [(a, b, c, d) for a in (0, 1) for b in (0, 1)
+                                               for c in (0, 1) for d in (0, 1)])
+@pytest.mark.parametrize("beta,lower,splitk", [(0.0, 0, 0), (1.0, 0, 1), (1.0, 1, 0), (0.0, 1, 1)])
+def test_gemm_beta01(L, ta, tb, tri_a, tri_b, beta, lower, splitk):
+    """beta in {0, 1} (the Cholesky / inverse products): every flag combination, a lower-triangular
+    C, split-K, and ragged sizes that cut every tile shape (128x128, 128x256, 256x128) and the
+    16-deep K tiles; C's entries outside the written region keep their garbage."""
+    m = 390 if not lower else 398
+    n = m if (lower or tri_b) else 302
+    k = m if tri_a else (n if tri_b else 278)
+    if tri_a and tri_b and not lower:
+        n = k = m
+    rng = np.random.default_rng(ta + 2 * tb + 4 * tri_a + 8 * tri_b + 16 * lower + 32 * splitk)
+    As = rng.standard_normal((k, m) if ta else (m, k))
+    Bs = rng.standard_normal((n, k) if tb else (k, n))
+    opA = (np.tril(As) if tri_a else As)
+    opB = (np.tril(Bs) if tri_b else Bs)
+    opA = opA.T if ta else opA
+    opB = opB.T if tb else opB
+    C0 = rng.standard_normal((m, n))
+    C = L.as_device(C0.copy())
+    L.gemm(As, Bs, C, alpha=-1.0, beta=beta, transa=bool(ta), transb=bool(tb), lower_c=bool(lower),
+           tri_a=bool(tri_a), tri_b=bool(tri_b), splitk=bool(splitk))
+    ref = -opA @ opB + beta * C0
+    got = C.cpu().numpy()
+    if lower:
+        il, iu = np.tril_indices(m), np.triu_indices(m, 1)
+        np.testing.assert_allclose(got[il], ref[il], rtol=1e-11, atol=1e-11)
+        assert np.array_equal(got[iu], C0[iu])
+    else:
+        np.testing.assert_allclose(got, ref, rtol=1e-11, atol=1e-11)
