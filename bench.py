@@ -334,8 +334,8 @@ def main():
         roof["traffic_vs_algorithmic"] = tr["bytes_per_launch"] / (nbytes / max(launches, 1))
         roof["traffic_source"] = tr["source"]
     elif dom == "gemm_f64":
-        roof["traffic_note"] = ("null: rocprofv3 --pmc segfaults when this workload dispatches "
-                                "gemm_glds_kernel<false,false,false,true> (profiles/README.md)")
+        roof["traffic_note"] = ("null: no PMC pass of this workload in " +
+                                os.path.relpath(args.traffic, ROOT) + " (tools/pmc_gemm_bench.sh)")
     # the HBM-bound kernel of the placement rounds, with its PMC-measured traffic
     ms_t, n_t, _, by_t = prof["greedy_trmv"]
     hbm = {"kernel": "greedy_trmv", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,

@@ -235,3 +235,20 @@ def test_gemm_beta01(L, ta, tb, tri_a, tri_b, beta, lower, splitk):
         assert np.array_equal(got[iu], C0[iu])
     else:
         np.testing.assert_allclose(got, ref, rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("tri_a,splitk", [(1, 1), (0, 1), (1, 0)])
+def test_gemm_bottom_right_block(L, tri_a, splitk):
+    """Operands and output are the bottom-right blocks of one large matrix (the trtri product
+    X21 = -X22 W of the last recursion level): no load may run past the last valid element."""
+    import torch
+    N, b = 2048, 512
+    rng = np.random.default_rng(5 + tri_a)
+    big = L.as_device(rng.standard_normal((N, N)))
+    W = L.as_device(rng.standard_normal((b, b)))
+    X22 = big[N - b:, N - b:]
+    C = big[N - b:, N - 2 * b:N - b]
+    ref = -(np.tril(X22.cpu().numpy()) if tri_a else X22.cpu().numpy()) @ W.cpu().numpy()
+    L.gemm(X22, W, C, alpha=-1.0, beta=0.0, tri_a=bool(tri_a), splitk=bool(splitk))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(C.cpu().numpy(), ref, rtol=1e-11, atol=1e-11)

@@ -651,12 +651,16 @@ __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(GemmParams p, int tiles
     const int k0 = (int)kbeg + GBK * tile;
     const double* base;
     int64_t rec;
+    // the range ends at the last valid element (not at the end of its row: the operand may be
+    // the bottom-right block of a larger matrix, with nothing allocated after it)
+    const int R = (int)(isA ? p.m : p.n);
     if (kc) {
       base = X + (int64_t)r0 * ld + min(k0, K);
-      rec = nrows * ld - min(k0, K);
+      rec = nrows > 0 ? (int64_t)(nrows - 1) * ld + (K - min(k0, K)) : 0;
     } else {
+      const int kr = min(GBK, K - min(k0, K));
       base = X + (int64_t)min(k0, K) * ld + r0;
-      rec = (int64_t)min(GBK, K - min(k0, K)) * ld - r0;
+      rec = kr > 0 ? (int64_t)(kr - 1) * ld + (R - r0) : 0;
     }
     // uniform by construction; readfirstlane keeps the resource in SGPRs (a VGPR resource
     // would turn every load into a waterfall loop)
@@ -1114,6 +1118,13 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     }
     ProfScope ps("gemm_f64", stream, fl,
                  8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    static const bool shapes = getenv("VGPOSP_PROF_SHAPES") != nullptr;
+    char shape_name[96];
+    if (shapes && prof_on())
+      snprintf(shape_name, sizeof(shape_name), "gemm:%lldx%lldx%lld:%c%c%c%c%c:s%d", (long long)m,
+               (long long)n, (long long)k, transa ? 'T' : 'N', transb ? 'T' : 'N',
+               uplo_c == VGPOSP_LOWER ? 'L' : 'F', tri_a ? 'a' : '-', tri_b ? 'b' : '-', p.nsplit);
+    ProfScope pshape(shape_name, stream, fl, 0.0, shapes && prof_on());
     dim3 g1((unsigned)(nblk * p.nsplit));
     if (FM == 4) launch_rs<4, 8>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     else launch_rs<8, 4>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
