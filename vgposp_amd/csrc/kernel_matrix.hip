@@ -4,7 +4,7 @@
 // ExponentiatedQuadratic, main_architecture_2_sampledistribution.py:211 MaternFiveHalves), which
 // TF evaluates by materialising an [n, m, d] squared-difference tensor.
 //
-// Layout: each 256-thread workgroup writes a 32-row x 128-column tile; lane pairs of columns are
+// Layout: each 256-thread workgroup writes a 128-row x 128-column tile; lane pairs of columns are
 // stored as one 16-byte write per row so a wave stores 1 KiB contiguous per row.  The X2 columns
 // of the tile are held in registers, X1 rows are wave-uniform (scalar-cached) loads.
 // Formula, as TFP evaluates it:  K = exp(2 log amp + log k(r / ls)).
@@ -13,21 +13,38 @@
 
 namespace vgposp {
 
-constexpr int KM_ROWS = 32;
+constexpr int KM_ROWS = 128;
 constexpr int KM_COLS = 128;
 constexpr int KM_MAXD = 8;
 
+__device__ __forceinline__ int km_tri_root(int64_t id) {
+  int64_t t = (int64_t)((sqrt(8.0 * (double)id + 1.0) - 1.0) * 0.5);
+  while ((t + 1) * (t + 2) / 2 <= id) ++t;
+  while (t * (t + 1) / 2 > id) --t;
+  return (int)t;
+}
+
+// One 128 x 128 tile per workgroup; a lower-triangular launch enumerates only the tiles on or
+// below the diagonal (blockIdx.x = ti (ti + 1) / 2 + tj).  Stores are non-temporal: K is far
+// larger than the caches and is next read by the factorization.
 template <int KIND, int D>
 __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, int64_t n1,
                                                             const double* X2, int64_t n2, int d,
                                                             const double* amp, const double* ls,
                                                             const double* diag_shift, int uplo,
                                                             double* K, int64_t ldk,
-                                                            int64_t stride_k, int vec) {
+                                                            int64_t stride_k, int vec,
+                                                            int tri_grid) {
   const int b = blockIdx.z;
-  const int64_t r0 = (int64_t)blockIdx.y * KM_ROWS;
-  const int64_t c0 = (int64_t)blockIdx.x * KM_COLS;
-  if (uplo == VGPOSP_LOWER && c0 > r0 + KM_ROWS - 1) return;
+  int64_t r0, c0;
+  if (tri_grid) {
+    const int ti = km_tri_root(blockIdx.x);
+    r0 = (int64_t)ti * KM_ROWS;
+    c0 = (int64_t)(blockIdx.x - ti * (ti + 1) / 2) * KM_COLS;
+  } else {
+    r0 = (int64_t)blockIdx.y * KM_ROWS;
+    c0 = (int64_t)blockIdx.x * KM_COLS;
+  }
   const int dd = D > 0 ? D : d;
   const double a = amp[b], l = ls[b];
   const double two_log_amp = 2.0 * log(a);
@@ -45,10 +62,9 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
     xa[k] = (k < dd && ca < n2) ? X2[ca * dd + k] : 0.0;
     xb[k] = (k < dd && cb < n2) ? X2[cb * dd + k] : 0.0;
   }
+  const int64_t rend = min(n1, r0 + KM_ROWS);
 #pragma unroll 2
-  for (int rr = 0; rr < KM_ROWS / 4; ++rr) {
-    const int64_t r = r0 + ty + 4 * rr;
-    if (r >= n1) break;
+  for (int64_t r = r0 + ty; r < rend; r += 4) {
     double da = 0.0, db = 0.0;
 #pragma unroll
     for (int k = 0; k < KM_MAXD; ++k) {
@@ -69,10 +85,11 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
     const bool oka = ca < n2 && (uplo != VGPOSP_LOWER || ca <= r);
     const bool okb = cb < n2 && (uplo != VGPOSP_LOWER || cb <= r);
     if (vec && oka && okb) {
-      *reinterpret_cast<double2*>(row + ca) = make_double2(va, vb);
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(d2v{va, vb}, reinterpret_cast<d2v*>(row + ca));
     } else {
-      if (oka) row[ca] = va;
-      if (okb) row[cb] = vb;
+      if (oka) __builtin_nontemporal_store(va, row + ca);
+      if (okb) __builtin_nontemporal_store(vb, row + cb);
     }
   }
 }
@@ -81,12 +98,12 @@ template <int KIND>
 static void launch_kind(dim3 g, hipStream_t s, const double* X1, int64_t n1, const double* X2,
                         int64_t n2, int d, const double* amp, const double* ls,
                         const double* shift, int uplo, double* K, int64_t ldk, int64_t stride,
-                        int vec) {
+                        int vec, int tri_grid) {
   switch (d) {
-    case 1: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 1>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
-    case 2: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 2>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
-    case 3: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 3>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
-    default: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 0>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec); break;
+    case 1: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 1>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
+    case 2: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 2>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
+    case 3: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 3>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
+    default: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 0>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
   }
 }
 
@@ -113,17 +130,22 @@ extern "C" int vgposp_kernel_matrix(int kind, const double* X1, int64_t n1, cons
   VG_CHECK_ARG(ldk >= n2, 13);
   VG_CHECK_ARG(batch == 1 || stride_k >= ldk * n1, 14);
   if (n1 == 0 || n2 == 0) return 0;
-  dim3 g((unsigned)ceil_div(n2, KM_COLS), (unsigned)ceil_div(n1, KM_ROWS), (unsigned)batch);
+  // a lower launch is square (n1 == n2 for the symmetric K): only the tiles on or below the diagonal
+  const int64_t tr = ceil_div(n1, KM_ROWS);
+  dim3 g = (uplo == VGPOSP_LOWER && n1 == n2)
+               ? dim3((unsigned)(tr * (tr + 1) / 2), 1u, (unsigned)batch)
+               : dim3((unsigned)ceil_div(n2, KM_COLS), (unsigned)tr, (unsigned)batch);
+  const int tri_grid = uplo == VGPOSP_LOWER && n1 == n2;
   const int vec = (reinterpret_cast<uintptr_t>(K) % 16 == 0) && (ldk % 2 == 0) &&
                   (batch == 1 || stride_k % 2 == 0);
   hipStream_t s = as_stream(stream);
   const double outs = (uplo == VGPOSP_LOWER) ? 0.5 * (double)n1 * (double)(n1 + 1) : (double)n1 * n2;
   ProfScope ps("kernel_matrix", s, 0.0, 8.0 * (batch * outs + (double)d * (n1 + n2)));
   switch (kind) {
-    case VGPOSP_KERNEL_EQ: launch_kind<VGPOSP_KERNEL_EQ>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
-    case VGPOSP_KERNEL_MATERN12: launch_kind<VGPOSP_KERNEL_MATERN12>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
-    case VGPOSP_KERNEL_MATERN32: launch_kind<VGPOSP_KERNEL_MATERN32>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
-    default: launch_kind<VGPOSP_KERNEL_MATERN52>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec); break;
+    case VGPOSP_KERNEL_EQ: launch_kind<VGPOSP_KERNEL_EQ>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec, tri_grid); break;
+    case VGPOSP_KERNEL_MATERN12: launch_kind<VGPOSP_KERNEL_MATERN12>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec, tri_grid); break;
+    case VGPOSP_KERNEL_MATERN32: launch_kind<VGPOSP_KERNEL_MATERN32>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec, tri_grid); break;
+    default: launch_kind<VGPOSP_KERNEL_MATERN52>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec, tri_grid); break;
   }
   VG_LAUNCH_CHECK();
   return 0;
