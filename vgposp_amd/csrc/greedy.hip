@@ -134,37 +134,60 @@ __global__ void greedy_extract_kernel(const double* M, int64_t n, int64_t lda,
 // part[rc][c] = sum_{r in chunk rc, r >= max(c, a)} M[r][c] * f(r, c)
 //   SQ: f = M[r][c]          (column norms: Q_cc = |M e_c|^2)
 //   else f = xcol[r]          (q = M^T x)
+// Each thread owns a column pair (one 16-byte load per row, non-temporal: L^-1 is streamed once
+// per round), four rows in flight; the pair's diagonal row contributes to its first column only.
+constexpr int TRMV_COLS = 2 * CT;  // columns per workgroup
+
+template <bool SQ>
+__device__ __forceinline__ double trmv_f(double m, const double* xcol, int64_t r) {
+  return SQ ? m * m : m * xcol[r];
+}
+
 template <bool SQ>
 __global__ __launch_bounds__(CT) void greedy_trmv_kernel(const double* M, int64_t n, int64_t lda,
                                                          const int64_t* selected, int round,
                                                          const double* xcol, double* part,
-                                                         int64_t cbeg, int64_t cend) {
-  const int64_t c0 = cbeg + (int64_t)blockIdx.x * CT;
+                                                         int64_t cbeg, int64_t cend, int vec) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const int64_t cb = (cbeg & ~(int64_t)1) + (int64_t)blockIdx.x * TRMV_COLS;
   const int64_t r0 = (int64_t)blockIdx.y * RC;
   const int64_t r1 = min(r0 + RC, n);
-  if (c0 >= r1) return;  // tile strictly above the diagonal: never read by the reducer
+  if (cb >= r1) return;  // tile strictly above the diagonal: never read by the reducer
   const int64_t a = SQ ? 0 : selected[round - 1];
-  const int64_t c = c0 + threadIdx.x;
-  double acc0 = 0.0, acc1 = 0.0;
-  if (c < cend) {
-    int64_t r = max(max(r0, a), c);
-    const double* p = M + r * lda + c;
-    for (; r + 1 < r1; r += 2, p += 2 * lda) {
-      const double m0 = p[0], m1 = p[lda];
-      if (SQ) {
-        acc0 += m0 * m0;
-        acc1 += m1 * m1;
-      } else {
-        acc0 += m0 * xcol[r];
-        acc1 += m1 * xcol[r + 1];
-      }
-    }
-    if (r < r1) {
-      const double m0 = p[0];
-      acc0 += SQ ? m0 * m0 : m0 * xcol[r];
-    }
-    part[blockIdx.y * n + c] = acc0 + acc1;
+  const int64_t c = cb + 2 * threadIdx.x;
+  if (c >= cend) return;
+  const bool two = c + 1 < cend;
+  double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;  // column c: s, column c + 1: t
+  int64_t r = max(max(r0, a), c);
+  if (r == c && r < r1) {  // diagonal of column c; (c, c + 1) is above the diagonal
+    s0 += trmv_f<SQ>(M[r * lda + c], xcol, r);
+    ++r;
   }
+  const double* p = M + r * lda + c;
+  if (vec && c + 1 < n) {
+    for (; r + 3 < r1; r += 4, p += 4 * lda) {
+      const d2v m0 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p));
+      const d2v m1 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p + lda));
+      const d2v m2 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p + 2 * lda));
+      const d2v m3 = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(p + 3 * lda));
+      s0 += trmv_f<SQ>(m0.x, xcol, r) + trmv_f<SQ>(m2.x, xcol, r + 2);
+      s1 += trmv_f<SQ>(m1.x, xcol, r + 1) + trmv_f<SQ>(m3.x, xcol, r + 3);
+      t0 += trmv_f<SQ>(m0.y, xcol, r) + trmv_f<SQ>(m2.y, xcol, r + 2);
+      t1 += trmv_f<SQ>(m1.y, xcol, r + 1) + trmv_f<SQ>(m3.y, xcol, r + 3);
+    }
+    for (; r < r1; ++r, p += lda) {
+      const d2v m0 = *reinterpret_cast<const d2v*>(p);
+      s0 += trmv_f<SQ>(m0.x, xcol, r);
+      t0 += trmv_f<SQ>(m0.y, xcol, r);
+    }
+  } else {
+    for (; r < r1; ++r, p += lda) {
+      s0 += trmv_f<SQ>(p[0], xcol, r);
+      if (c + 1 < n) t0 += trmv_f<SQ>(p[1], xcol, r);
+    }
+  }
+  if (c >= cbeg) part[blockIdx.y * n + c] = s0 + s1;
+  if (two) part[blockIdx.y * n + c + 1] = t0 + t1;
 }
 
 // denom = conditional variance of y given V \ (A u {y}) with eps on that block's diagonal:
@@ -444,10 +467,11 @@ extern "C" int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int 
   int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_fact_ws(ws, w, n), s);
   if (rc) return rc;
   // Q_ii = |M e_i|^2 -> part (reduced in the round-0 update)
-  dim3 g((unsigned)ceil_div(n, CT), (unsigned)ceil_div(n, RC));
+  dim3 g((unsigned)ceil_div(n, TRMV_COLS), (unsigned)ceil_div(n, RC));
+  const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);
   ProfScope ps("greedy_colsq", s, (double)n * (n + 1), 8.0 * (0.5 * (double)n * (n + 1) + (double)ceil_div(n, RC) * n));
   hipLaunchKernelGGL(greedy_trmv_kernel<true>, g, dim3(CT), 0, s, Sigma, n, lda, nullptr, 0,
-                     nullptr, w.part, (int64_t)0, n);
+                     nullptr, w.part, (int64_t)0, n, vec);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -492,12 +516,13 @@ extern "C" int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda,
     hipLaunchKernelGGL(greedy_extract_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
                        Sigma, n, lda, selected, round, w.xcol);
     VG_LAUNCH_CHECK();
-    dim3 g((unsigned)ceil_div(c1 - c0, CT), (unsigned)ceil_div(n, RC));
+    dim3 g((unsigned)ceil_div(c1 - (c0 & ~(int64_t)1), TRMV_COLS), (unsigned)ceil_div(n, RC));
+    const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);
     // algorithmic: the lower triangle of L^-1 in rows >= a, columns [c0, c1) (a is device-side;
     // bench.py recomputes the exact bytes from the selections)
     ProfScope ps("greedy_trmv", s, 0.0, 8.0 * (0.5 * (double)n * (n + 1) + 2.0 * n));
     hipLaunchKernelGGL(greedy_trmv_kernel<false>, g, dim3(CT), 0, s, Sigma, n, lda, selected,
-                       round, w.xcol, w.part, c0, c1);
+                       round, w.xcol, w.part, c0, c1, vec);
     VG_LAUNCH_CHECK();
   }
   {
