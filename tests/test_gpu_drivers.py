@@ -40,3 +40,21 @@ def test_main_placement_pipeline(tmp_path):
     # main.py:575: the LML surface at the fitted noise
     ref_H = ogp.calc_H("matern12", X[tr], y[tr], r["noise"], 8, 6)
     np.testing.assert_allclose(r["H"], ref_H, rtol=1e-8)
+
+
+def test_main_architecture_2_pipeline(tmp_path):
+    import main_architecture_2 as arch2
+    cover, k = (4, 4, 4), 6
+    r = arch2.run(cover=cover, n_obs=2048, m=3, batch=256, steps=20, k=k, cutoff=1,
+                  out_dir=str(tmp_path))
+    assert np.isfinite(r["losses"]).all() and r["losses"][-1] < r["losses"][0]
+    # cov_vv over the T/P samples of the VGP tracer field, then the beta-decay filter
+    np.testing.assert_allclose(r["cov_raw"], ocov.empirical_cov(r["T"]), rtol=1e-9, atol=1e-13)
+    np.testing.assert_allclose(r["cov_vv"], ocov.index_taper(r["cov_raw"], cover, arch2.BETA_val),
+                               rtol=1e-12, atol=1e-15)
+    # arch2:871 and the windowed variant: exact selections vs the restated TF graphs
+    _, _, _, ref_sel = op.sparse_placement_algorithm_2(r["cov_vv"], k, cover)
+    assert r["alg2"] == [int(v) for v in ref_sel[:, 0]]
+    ref3, _, _ = op.sparse_placement_algorithm_3(r["cov_vv"], k, cover, 1)
+    assert r["alg3_set"] == sorted(int(v) for v in ref3)
+    assert (tmp_path / "selection.csv").stat().st_size > 0
