@@ -79,3 +79,25 @@ def test_k_equals_n_and_tiny(P):
     assert [int(a) for a in P.placement_algorithm_2(np.array([[2.0]]), 1)] == [0]
     with pytest.raises(ValueError):
         P.placement_algorithm_2(cov, 5)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_singular_cov_matches_pinv(seed):
+    """A singular cov_vv (duplicated locations; and an empirical covariance with fewer samples
+    than locations, main.py:125-350): the reference's pinv defines every delta; the device path
+    retries with a relative jitter and must pick the same sensors."""
+    from oracle import gp as ogp
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    from vgposp_amd.placement_algorithm2 import placement_algorithm_2
+    X = grid_points((4, 4, 4), jitter=0.05, seed=seed)
+    C = ogp.kernel_matrix("eq", X, X, 1.0, 2 * grid_spacing((4, 4, 4)))[0] + 0.01 * np.eye(len(X))
+    dup = [5, 17, 40]
+    C = np.concatenate([C, C[dup]], 0)
+    C = np.concatenate([C, C[:, dup]], 1)
+    assert [int(a) for a in placement_algorithm_2(C, 8)] == \
+        [int(a) for a in op.placement_algorithm_2(C, 8)]
+    rng = np.random.default_rng(seed)
+    T = rng.standard_normal((48, 20))
+    E = (T - T.mean(1, keepdims=True)) @ (T - T.mean(1, keepdims=True)).T / 20
+    assert [int(a) for a in placement_algorithm_2(E, 5)] == \
+        [int(a) for a in op.placement_algorithm_2(E, 5)]

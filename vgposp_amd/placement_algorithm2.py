@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from . import linalg
-from ._lib import call, query
+from ._lib import CholeskyError, call, query
 from .linalg import _p, _stream
 
 
@@ -99,11 +99,32 @@ class GreedyPlacement:
                 self.evals[: self.rounds].cpu().numpy())
 
 
+# A singular (PSD, not PD) cov_vv, e.g. an empirical covariance with fewer samples than locations
+# (main.py:125-350): the reference's pinv still defines every delta.  The device path then factors
+# Sigma + eps I with a relative eps and takes denom = 1 / P_yy - eps (vgposp_greedy_init_ex's
+# jitter), so a candidate in the span of the others gets denom ~ 0 -> delta 0 at the 1e-8
+# threshold, as with pinv, and every other delta moves by O(eps).
+SINGULAR_EPS = (1e-12, 1e-10, 1e-8)
+
+
 def _place(cov_vv, k, lazy, verbose):
     if k < 1:
         return []
-    g = GreedyPlacement(cov_vv, k, copy=True).run(k, lazy=lazy)
-    A, deltas, _ = g.result()
+    try:
+        g = GreedyPlacement(cov_vv, k, copy=True).run(k, lazy=lazy)
+        A, deltas, _ = g.result()
+    except CholeskyError as err:
+        S = linalg.as_device(cov_vv)
+        scale = float(torch.mean(torch.diagonal(S)).abs()) or 1.0
+        for rel in SINGULAR_EPS:
+            try:
+                g = GreedyPlacement(S, k, copy=True, jitter=rel * scale).run(k, lazy=lazy)
+                A, deltas, _ = g.result()
+                break
+            except CholeskyError:
+                continue
+        else:
+            raise err
     if verbose:
         for y, d in zip(A, deltas):
             print("y*=", y, "delta=", d)
