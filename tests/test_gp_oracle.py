@@ -105,3 +105,21 @@ def test_vgp_training_grads_match_finite_differences(kind, adjoint):
             Zm[i, k] -= h
             fz[i, k] = (f(a, l, s, Zp) - f(a, l, s, Zm)) / (2 * h)
     np.testing.assert_allclose(gZ, fz, rtol=1e-5, atol=1e-6 * np.abs(fz).max())
+
+
+def test_data_generation_helpers():
+    """data_generation.py:24-122 restated: shapes, ranges and the polynomial columns."""
+    from vgposp_amd import data_generation as dg
+    rng = np.random.default_rng(0)
+    P = dg.generate_random_points(100, [-2.0, 2.0], rng)
+    assert P.shape == (100, 2) and P.min() >= -2.0 and P.max() < 2.0
+    assert np.array_equal(dg.create_line(np.array([3.0, 1.0, 2.0]), np.array([1.0, 1.0, 0.5])),
+                          [2.0, 0.0, 1.5])
+    for deg, f in ((6, dg.generate_6d_polinomials), (4, dg.generate_4d_polinomials)):
+        D = f(np.random.default_rng(1))
+        assert D.shape == (1200, deg)
+        np.testing.assert_allclose(D, D[:, :1] ** np.arange(1, deg + 1), rtol=1e-15)
+    X, y = dg.generate_noisy_2Dsin_data(50, 1e-3, [[-2, 2], [-1, 1]], np.random.default_rng(2))
+    assert X.shape == (50, 2) and y.shape == (50,) and (np.abs(X[:, 1]) <= 1).all()
+    C = dg.create_random_cov(7, np.random.default_rng(3))
+    assert np.allclose(C, C.T) and np.linalg.eigvalsh(C).min() > -1e-12

@@ -73,6 +73,31 @@ def generate_noisy_1Dsin_data(num_train_pts, obs_noise_variance, coord_range, rn
     return idx_pts, sinusoid(idx_pts) + noise
 
 
+def generate_random_points(num_pts, range_val, rng=None):
+    """data_generation.py:82-84 — (num_pts, 2) uniform points in [range_val[0], range_val[1])."""
+    return _rng(rng).uniform(range_val[0], range_val[1], size=(num_pts, 2))
+
+
+def create_line(u, v):
+    """data_generation.py:87-89."""
+    return np.asarray(u) - np.asarray(v)
+
+
+def _polynomial_columns(degree, num=1200, rng=None):
+    col = _rng(rng).uniform(size=(num, 1))
+    return np.concatenate([col ** p for p in range(1, degree + 1)], axis=1).astype(np.float64)
+
+
+def generate_6d_polinomials(rng=None):
+    """data_generation.py:98-109 — rows (o, o^2, ..., o^6), o ~ U(0, 1), 1200 rows."""
+    return _polynomial_columns(6, rng=rng)
+
+
+def generate_4d_polinomials(rng=None):
+    """data_generation.py:112-122 — rows (o, o^2, o^3, o^4), o ~ U(0, 1), 1200 rows."""
+    return _polynomial_columns(4, rng=rng)
+
+
 def create_random_cov(n, rng=None):
     """data_generation.py:92-95 — U U^T with U ~ U(0,1)^{n x n}."""
     m = _rng(rng).uniform(0, 1, n ** 2).reshape(-1, n)
