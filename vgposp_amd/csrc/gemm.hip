@@ -3,13 +3,17 @@
 //
 //   C = alpha * op(A) * op(B) + beta * C        (row-major, fp64)
 //
-// Tiling: 128x128 output tile per 256-thread workgroup (4 waves in a 2x2 grid, 64x64 = 4x4 MFMA
-// fragments per wave), BK = 16, two LDS buffers with register staging (global loads of tile t+1
-// are in flight while tile t is multiplied).  Operands are staged in one of two LDS images, both
-// bank-conflict-free for the MFMA fragment reads (lane l reads row l&15, k = l>>4):
-//   KC image [row][k] with a row pitch of 18 doubles   (operand stored k-contiguous)
-//   MC image [k][row] with a row pitch of 144 doubles  (operand stored row-contiguous)
-// so no operand ever needs an explicit transpose in HBM.
+// Three kernels share the 128x128x16 tile geometry (4 waves in a 2x2 grid, 64x64 = 4x4 MFMA
+// fragments per wave):
+//   gemm_glds_kernel (default)  LDS-DMA staging (global_load_lds), 2-stage ring, 2 WG per CU,
+//                               XOR-swizzled lane-linear LDS images; described above the kernel.
+//   gemm_rs_kernel (opt-in)     one wave per SIMD, register-staged, 256 AGPR accumulators.
+//   gemm_ref_kernel (fallback)  odd sizes / unaligned operands: register staging into padded
+//                               images, bank-conflict-free for the fragment reads (lane l reads
+//                               row l&15, k = l>>4):
+//     KC image [row][k] with a row pitch of 18 doubles   (operand stored k-contiguous)
+//     MC image [k][row] with a row pitch of 144 doubles  (operand stored row-contiguous)
+// No operand ever needs an explicit transpose in HBM.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
