@@ -308,7 +308,16 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   constexpr int PO = 16 / NW;                          // pieces per operand per wave
   constexpr int PPW = PO * (NSUB + 1);                 // pieces per wave per stage (8, 12 or 6)
   constexpr bool SPREAD = NST >= 3;                    // next-tile loads between the MFMAs
-  __shared__ double smem[NST * SE];
+#if VGPOSP_GEMM_B128
+  // b128 fragment reads (experiment): lane group fk covers k = 4 fk + s (s = 0..3), so a KC
+  // operand's substeps 2h and 2h + 1 are one 16-byte pair; an MC operand's 16-byte pair is two
+  // adjacent rows of one k, i.e. fragments 2g and 2g + 1 (rows 32 g + 2 x + {0, 1}).
+  constexpr bool B128 = NST == 2;
+#else
+  constexpr bool B128 = false;
+#endif
+  constexpr bool A_IL = B128 && !A_KC, B_IL = B128 && !B_KC;  // row-interleaved fragments
+  __shared__ __attribute__((aligned(16))) double smem[NST * SE];
 
   // Tile order.  Uniform-K launches: XCD-aware bijective remap (each XCD walks a contiguous range
   // of tiles, so neighbours share A rows / B columns in its L2).  A lower-triangular A (K range
@@ -433,6 +442,68 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     // of a triangular operand (k0 within 128 of the tile's first row / column)
     const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + TBM && k0 + GBK > m0) ||
                       (TRIB && k0 < n0 + GBN && k0 + GBK > n0);
+    if constexpr (B128) {
+      // x[e][f]: substep 2h + e of fragment f; rb = the wave's first row of the operand image
+      auto frags = [&](auto kc, const double* X, int rb, auto nf, int h, double (&x)[2][decltype(nf)::value]) {
+        constexpr int F = decltype(nf)::value;
+        if constexpr (decltype(kc)::value) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            const int r = rb + f * 16 + fr;
+            const double2 v = *reinterpret_cast<const double2*>(X + r * 16 + 2 * ((2 * fk + h) ^ ((r & 15) >> 1)));
+            x[0][f] = v.x;
+            x[1][f] = v.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int k = 4 * fk + 2 * h + e;
+#pragma unroll
+            for (int g = 0; g < F / 2; ++g) {
+              const int pr = (rb >> 1) + 16 * g + fr;
+              const double2 v = *reinterpret_cast<const double2*>(X + k * 128 + 2 * (pr ^ ((k & 1) << 3)));
+              x[e][2 * g] = v.x;
+              x[e][2 * g + 1] = v.y;
+            }
+          }
+        }
+      };
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double a[2][FI], b[2][4];
+        frags(std::integral_constant<bool, A_KC>{}, As, (wm * WROWS) % GBM, std::integral_constant<int, FI>{}, h, a);
+        frags(std::integral_constant<bool, B_KC>{}, Bs, wn * 64, std::integral_constant<int, 4>{}, h, b);
+        if (mask) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int64_t gk = k0 + 4 * fk + 2 * h + e;
+#pragma unroll
+            for (int i = 0; i < FI; ++i) {
+              const int64_t gm = m0 + wm * WROWS + (A_IL ? 32 * (i >> 1) + 2 * fr + (i & 1) : i * 16 + fr);
+              if (gk >= kend || (TRIA && (TA ? gm > gk : gk > gm))) a[e][i] = 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int64_t gn = n0 + wn * 64 + (B_IL ? 32 * (j >> 1) + 2 * fr + (j & 1) : j * 16 + fr);
+              if (gk >= kend || (TRIB && (TB ? gk > gn : gn > gk))) b[e][j] = 0.0;
+            }
+          }
+        }
+#ifdef VGPOSP_GEMM_EXP_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e][i], b[e][j], acc[i][j], 0, 0, 0);
+#ifdef VGPOSP_GEMM_EXP_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      }
+    } else
 #pragma unroll
     for (int ks = 0; ks < GBK / 4; ++ks) {
       const int k = ks * 4 + fk;
@@ -464,11 +535,17 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
 #pragma unroll
         for (int q = (ks * PPW) / 4; q < ((ks + 1) * PPW) / 4; ++q) issue_piece(t + NST - 1, q);
       }
+#ifdef VGPOSP_GEMM_EXP_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+#ifdef VGPOSP_GEMM_EXP_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   }
 
@@ -477,10 +554,11 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   for (int i = 0; i < FI; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 16 + fr;
+      const int64_t col = n0 + wn * 64 + (B_IL ? 32 * (j >> 1) + 2 * fr + (j & 1) : j * 16 + fr);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * WROWS + i * 16 + fk + 4 * r;
+        const int x = fk + 4 * r;
+        const int64_t row = m0 + wm * WROWS + (A_IL ? 32 * (i >> 1) + 2 * x + (i & 1) : i * 16 + x);
         if (row < p.m && col < p.n && (!lower || col <= row)) {
           if (p.nsplit > 1) {
             p.part[(int64_t)zsplit * p.m * p.n + row * p.n + col] = p.alpha * acc[i][j][r];
