@@ -238,6 +238,9 @@ __global__ __launch_bounds__(256) void gemm_ref_kernel(GemmParams p, int vec_a, 
 #ifndef VGPOSP_GEMM_STAGES
 #define VGPOSP_GEMM_STAGES 2
 #endif
+#ifndef VGPOSP_GEMM_GROUP
+#define VGPOSP_GEMM_GROUP 4
+#endif
 #ifndef VGPOSP_GEMM_OCC
 #define VGPOSP_GEMM_OCC 2
 #endif
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     ti = tri_root(wg);
     tj = wg - ti * (ti + 1) / 2;
   } else {
-    constexpr int GROUP = 8;  // row tiles per group: neighbours share A rows and B columns
+    constexpr int GROUP = VGPOSP_GEMM_GROUP;  // row tiles per group: neighbours share A rows and B columns
     const int per_group = GROUP * tiles_n;
     const int g = wg / per_group, first = g * GROUP;
     const int gsize = min(GROUP, tiles_m - first);
