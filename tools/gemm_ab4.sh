@@ -1,9 +1,9 @@
 #!/bin/bash
 # A/B of the GEMM tile-group size (row tiles per XCD band): the 16384^3 layout sweep and the
-# 65k placement step for the default build (GROUP 8) and tools/variants/lib_group{4,16}.so
+# 65k placement step for the default build and each tools/variants/lib_group*.so
 set -e
 cd ${GRAFT_REPO_ROOT:-$PWD}; mkdir -p gpurun_out
-for lib in default tools/variants/lib_group4.so tools/variants/lib_group16.so; do
+for lib in default tools/variants/lib_group*.so; do
   if [ $lib = default ]; then unset VGPOSP_LIB; else export VGPOSP_LIB=$PWD/$lib; fi
   echo "== $lib" >> gpurun_out/ab4_layouts.txt
   timeout -k 10 300 python -u tools/gemm_layouts.py >> gpurun_out/ab4_layouts.txt 2>&1
