@@ -19,6 +19,4 @@ Contents
                ``VariationalGaussianProcess``.  TF/TFP are absent from this container and no
                reference test pins numbers at that boundary, so these are **parity unpinned**
                except the exact-GP LML, which is cross-checked against scikit-learn.
-``cblas``      plain-C restatement (``oracle/c/``) of kernel assembly + Cholesky used as a second,
-               independent checker and as the bounded CPU baseline.
 """

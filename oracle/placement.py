@@ -220,6 +220,76 @@ def placement_lazy_precision(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, ca
     return A
 
 
+def _lazy_select_np(cache, fresh_delta, selected):
+    """lazy_select with numpy scans (same decisions: the first maximum of the non-selected cache
+    is the lowest index among ties, placement_algorithm2.py:53-67; NaN never wins)."""
+    uptodate = np.zeros(len(cache), dtype=bool)
+    evaluated = []
+    while True:
+        c = np.where(selected | np.isnan(cache), -np.inf, cache)
+        y = int(np.argmax(c))
+        if uptodate[y]:
+            return y, evaluated
+        cache[y] = fresh_delta[y]
+        uptodate[y] = True
+        evaluated.append(y)
+
+
+def placement_lazy_incremental(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, cache_init=np.inf,
+                               deltas_out=None):
+    """placement_lazy_precision with O(N^3) once + O(N^2) per round, for N ~ 16k (the GPU test of a
+    full k = 50 sequence).  Same deltas, rank-1 updated instead of re-factored:
+      nom_y  = sigma_yy - |W[:, y]|^2,  W[t] = (Sigma_{a_t,:} - W^T W[:, a_t]) / sqrt(pivot_t)
+               (pivot_t = sigma_{a_t a_t} + eps - |W[:, a_t]|^2: Cholesky of Sigma_AA + eps I);
+      P_yy   = Q_yy - |V[:, y]|^2,  Q = (Sigma + eps I)^-1,  V[t] = (Q e_{a_t} - V^T V[:, a_t]) /
+               sqrt(P_{a_t a_t}): removing a_t from S = V \\ A downdates (Sigma_SS + eps I)^-1;
+      denom_y = 1 / P_yy - eps.
+    Pinned against placement_lazy_precision and the reference goldens in tests/test_oracle.py."""
+    from scipy.linalg import lapack
+    cov = np.asarray(cov_vv, dtype=np.float64)
+    N = cov.shape[0]
+    Mj = cov.copy()
+    Mj[np.diag_indices(N)] += jitter
+    c, info = lapack.dpotrf(Mj, lower=1, clean=0, overwrite_a=1)
+    if info != 0:
+        raise np.linalg.LinAlgError(f"dpotrf info {info}")
+    Q, info = lapack.dpotri(c, lower=1, overwrite_c=1)
+    if info != 0:
+        raise np.linalg.LinAlgError(f"dpotri info {info}")
+    del c, Mj
+    Q = np.tril(Q) + np.tril(Q, -1).T
+    diag = np.diag(cov).copy()
+    nom = diag.copy()
+    prec = np.diag(Q).copy()
+    W = np.zeros((k, N))
+    V = np.zeros((k, N))
+    cache = np.full(N, float(cache_init))
+    selected = np.zeros(N, dtype=bool)
+    A = []
+    for r in range(k):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            den = 1.0 / prec - jitter
+            ok = (np.abs(nom) >= thr) & (np.abs(den) >= thr)
+            delta = np.where(ok, nom / den, 0.0)
+        delta[selected] = np.nan
+        if lazy:
+            y, _ = _lazy_select_np(cache, delta, selected)
+        else:
+            d = np.where(selected | np.isnan(delta), -np.inf, delta)
+            y = int(np.argmax(d))
+        if deltas_out is not None:
+            deltas_out.append(float(delta[y]))
+        A.append(y)
+        selected[y] = True
+        w = (cov[y] - W[:r].T @ W[:r, y]) / np.sqrt(diag[y] + jitter - W[:r, y] @ W[:r, y])
+        W[r] = w
+        nom = nom - w * w
+        v = (Q[y] - V[:r].T @ V[:r, y]) / np.sqrt(prec[y])
+        V[r] = v
+        prec = prec - v * v
+    return A
+
+
 # ---------------------------------------------------------------------------------------------
 # The TF-graph variant: snippets_a2.sparse_placement_algorithm_2 (snippets_a2.py:679-822).
 # TensorFlow is absent, so this is a restatement from the source (parity unpinned by execution);

@@ -1,0 +1,116 @@
+"""GPU parity at BASELINE.json's config sizes (C2, C3, C5) and a full k = 50 placement sequence at
+N = 16,384 against the oracle run on the box's CPU.
+
+* C2: 32^3 grid (N = 32,768), EQ amp 1 ls 2h, noise 1e-2 + 1e-6: lower-triangle assembly + the
+  plain potrf.  L L^T z = Sigma z and Sigma L^-T L^-1 z = z on random probes (Sigma assembled again
+  in full), ldiag = diag(L), and the log-det of the leading 4,096 block (a Cholesky's leading block
+  is the leading block's Cholesky) against numpy.
+* C3 (64^3 obs, M = 512, B = 32,768) and C5 (65,536 x 5-D obs, M = 1,024, B = 8,192): the training
+  objective -ELBO and its gradient w.r.t. (amp, ls, noise, Z) against
+  ``oracle.gp.vgp_training_loss_grads`` at the reference's initial trainables
+  (variational_Gaussian_process_example.py:51-64).  Tolerance: loss 1e-8 relative (north_star asks
+  1e-5), gradients 1e-6 relative to the largest component.
+* N = 16,384 (32 x 32 x 16 jittered grid): the 50 lazy-greedy picks of placement_algorithm_2
+  (placement_algorithm2.py:151-219) equal ``oracle.placement.placement_lazy_incremental`` on the
+  same device-assembled Sigma, index for index; the selected deltas agree to 1e-9.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gp as ogp
+from oracle import placement as op
+
+pytestmark = pytest.mark.gpu
+
+
+def _sp(v):
+    return float(np.log1p(np.exp(v)))
+
+
+def test_c2_assembly_and_potrf():
+    from vgposp_amd import linalg
+    from vgposp_amd.workloads import c2_data
+    torch.cuda.set_device(0)
+    X, ls = c2_data()
+    n = len(X)
+    shift = 1e-2 + 1e-6
+    Xd = linalg.as_device(X)
+    A = linalg.kernel_matrix("eq", Xd, None, 1.0, ls, diag_shift=shift, lower=True)[0]
+    _, ldiag, info = linalg.cholesky_(A, invert=False)
+    ldiag = ldiag[0]
+    assert torch.equal(ldiag, torch.diagonal(A))
+    Sig = linalg.kernel_matrix("eq", Xd, None, 1.0, ls, diag_shift=shift)[0]
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    Z = torch.randn(n, 4, dtype=torch.float64, device="cuda", generator=gen)
+    # forward: L (L^T Z) = Sigma Z
+    LtZ = linalg.gemm(A, Z, transa=True, tri_a=True)
+    LLtZ = linalg.gemm(A, LtZ, tri_a=True)
+    SZ = Sig @ Z
+    assert float((LLtZ - SZ).norm() / SZ.norm()) < 1e-13
+    # inverse: Sigma L^-T L^-1 Z = Z
+    W = linalg.trsm(A, linalg.trsm(A, Z), trans=True)
+    assert float((Sig @ W - Z).norm() / Z.norm()) < 1e-8
+    # log-det of the leading block against numpy's Cholesky of the same entries
+    m = 4096
+    S11 = Sig[:m, :m].cpu().numpy()
+    ld_ref = 2.0 * np.sum(np.log(np.diag(np.linalg.cholesky(S11))))
+    ld = 2.0 * float(torch.log(ldiag[:m]).sum())
+    assert ld == pytest.approx(ld_ref, rel=1e-12)
+    assert bool(torch.all(ldiag > 0))
+    del A, Sig
+    torch.cuda.empty_cache()
+
+
+def _vgp_case(which):
+    from vgposp_amd import linalg
+    from vgposp_amd.vgp_training import VGPObjective
+    from vgposp_amd.workloads import vgp_c3_data, vgp_c5_data
+    torch.cuda.set_device(0)
+    X, y, Z = vgp_c3_data() if which == "c3" else vgp_c5_data()
+    N = len(X)
+    B = N // 8
+    bi = np.random.default_rng(3).integers(0, N, B)
+    a, l, s = _sp(0.54), 1e-5 + _sp(0.54), _sp(0.54)
+    obj = VGPObjective("eq", X, y)
+    dev = lambda v: torch.tensor(v, dtype=torch.float64, device="cuda")  # noqa: E731
+    E, ga, gl, gs, gZ = obj.loss_and_grads(linalg.as_device(Z), dev(a), dev(l), dev(s),
+                                           linalg.as_device(X[bi]), linalg.as_device(y[bi]), B / N)
+    got = (float(E), float(ga), float(gl), float(gs), gZ.cpu().numpy())
+    ref = ogp.vgp_training_loss_grads("eq", Z, X, y, X[bi], y[bi], a, l, s, B / N)
+    assert got[0] == pytest.approx(ref[0], rel=1e-8)
+    scale = max(abs(ref[1]), abs(ref[2]), abs(ref[3]), float(np.abs(ref[4]).max()))
+    for g, r in zip(got[1:4], ref[1:4]):
+        assert abs(g - r) <= 1e-6 * scale, (g, r)
+    np.testing.assert_allclose(got[4], ref[4], rtol=0, atol=1e-6 * scale)
+
+
+@pytest.mark.timeout(400)
+def test_c3_vgp_loss_and_grads_vs_oracle():
+    _vgp_case("c3")
+
+
+@pytest.mark.timeout(400)
+def test_c5_vgp_loss_and_grads_vs_oracle():
+    _vgp_case("c5")
+
+
+@pytest.mark.timeout(400)
+def test_k50_sequence_at_16k_vs_oracle():
+    from vgposp_amd import linalg
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    torch.cuda.set_device(0)
+    shape = (32, 32, 16)
+    X = grid_points(shape, jitter=0.05, seed=7)
+    ls = 2 * grid_spacing(shape)
+    S = linalg.kernel_matrix("eq", X, None, 1.0, ls, diag_shift=1e-2 + 1e-6)[0]
+    cov = S.cpu().numpy()
+    g = GreedyPlacement(S, 50).run()
+    sel, dlt, _ = g.result()
+    ref_d = []
+    ref = op.placement_lazy_incremental(cov, 50, deltas_out=ref_d)
+    assert [int(a) for a in sel] == ref
+    np.testing.assert_allclose(dlt, ref_d, rtol=1e-9)
+    del S, g
+    torch.cuda.empty_cache()

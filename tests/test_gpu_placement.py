@@ -101,3 +101,39 @@ def test_singular_cov_matches_pinv(seed):
     E = (T - T.mean(1, keepdims=True)) @ (T - T.mean(1, keepdims=True)).T / 20
     assert [int(a) for a in placement_algorithm_2(E, 5)] == \
         [int(a) for a in op.placement_algorithm_2(E, 5)]
+
+
+@pytest.mark.parametrize("seed", [179, 211])
+def test_near_singular_cov_takes_jitter_path(seed):
+    """Centred 24 x 23 samples (rank 22): the Cholesky can succeed with a rounding-level pivot
+    (advisor finding, round 1).  The relative pivot check sends it to the jitter path, whose picks
+    equal the reference's pinv picks."""
+    from vgposp_amd.placement_algorithm2 import placement_algorithm_2
+    rng = np.random.default_rng(seed)
+    T = rng.standard_normal((24, 23))
+    Tc = T - T.mean(1, keepdims=True)
+    E = Tc @ Tc.T / 23
+    assert [int(a) for a in placement_algorithm_2(E, 6)] == \
+        [int(a) for a in op.placement_algorithm_2(E, 6)]
+
+
+@pytest.mark.parametrize("name", ["grid5", "grid654", "spd40", "grid8", "grid4"])
+def test_trace_matches_reference_print_lines(P, name, capsys):
+    """The per-evaluation records (placement_algorithm2.py:205 'delta_y= .. y_st= ..' and :188
+    'y*= ..') against the reference's own printed trace: same candidates in the same order, same
+    deltas to 1e-9."""
+    e = CASES[name]
+    trace = []
+    A = P.placement_algorithm_2(placement_cov(name, e), e["k"], trace=trace)
+    assert [int(a) for a in A] == e["alg2"]
+    ref = [tuple(t) for t in e["trace"]]
+    assert [t[0] for t in trace] == [t[0] for t in ref]
+    for got, exp in zip(trace, ref):
+        if got[0] == "select":
+            assert got[1] == exp[1]
+        else:
+            assert got[1] == pytest.approx(exp[1], rel=1e-9, abs=1e-12)
+    P.placement_algorithm_2(placement_cov(name, e), e["k"], verbose=True)
+    lines = capsys.readouterr().out.splitlines()
+    assert len(lines) == len(ref)
+    assert lines[-1] == f"y*= {e['alg2'][-1]}"

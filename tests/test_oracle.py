@@ -55,3 +55,25 @@ def test_precision_deltas_match_trace(name):
             pos += 1
         A.append(trace[pos][1])
         pos += 1
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_incremental_oracle_matches_reference(name):
+    """The O(N^2)-per-round restatement (used by the GPU test at N = 16k) against the goldens."""
+    e = CASES[name]
+    cov = placement_cov(name, e)
+    assert op.placement_lazy_incremental(cov, e["k"]) == e["alg2"]
+    if "alg1" in e:
+        assert op.placement_lazy_incremental(cov, e["k"], lazy=False) == e["alg1"]
+
+
+@pytest.mark.parametrize("jitter,thr,cinit", [(0.0, 1e-8, np.inf), (1e-6, 1e-7, 1e8)])
+def test_incremental_oracle_matches_precision(jitter, thr, cinit):
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    from oracle import gp as ogp
+    shape = (9, 8, 7)
+    X = grid_points(shape, jitter=0.05, seed=11)
+    K = ogp.kernel_matrix("matern32", X, X, 1.0, 2 * grid_spacing(shape))[0] + 0.01 * np.eye(len(X))
+    a = op.placement_lazy_incremental(K, 20, jitter=jitter, thr=thr, cache_init=cinit)
+    b = op.placement_lazy_precision(K, 20, jitter=jitter, thr=thr, cache_init=cinit)
+    assert a == b

@@ -51,7 +51,9 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // (value, index) arg-max with the reference's tie rule: larger value wins; on equal value the
 // LOWER index wins (placement_algorithm2.py:62 uses strict '<' scanning upward).  Index -1 is
-// "no candidate" and loses to everything.  NaN values never win (comparisons are false).
+// "no candidate" and loses to everything.  A NaN value ranks below every number (the reference's
+// `delta_st < delta_y` is false for NaN, so a NaN delta is never selected), which keeps key_gt a
+// strict order whatever the lane order of a reduction.
 struct KeyMax {
   double v;
   long long i;
@@ -60,6 +62,8 @@ struct KeyMax {
 __device__ __forceinline__ bool key_gt(double v1, long long i1, double v2, long long i2) {
   if (i1 < 0) return false;
   if (i2 < 0) return true;
+  if (__builtin_isnan(v1)) return __builtin_isnan(v2) && i1 < i2;
+  if (__builtin_isnan(v2)) return true;
   return (v1 > v2) || (v1 == v2 && i1 < i2);
 }
 

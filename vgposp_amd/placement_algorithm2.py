@@ -89,6 +89,27 @@ class GreedyPlacement:
             self.step(lazy)
         return self
 
+    def step_traced(self, trace):
+        """A lazy step() that also appends the reference's per-evaluation records to ``trace``: one
+        ``(y, delta_y)`` per delta evaluated this round, in the reference's order, then
+        ``('select', y*)`` — what placement_algorithm2.py:205 and :188 print.
+
+        The lazy loop (:183-208) evaluates the stale cache entries in descending key order (value,
+        then lower index) and stops at the first fresh arg-max, so the evaluated entries are the
+        first ``evals[r]`` of the pre-round cache sorted by key, and their deltas are the
+        post-round cache values.  The device makes every decision; this only reads back the two
+        cache states and the evaluation count."""
+        r = self.rounds
+        cache = self.cache()
+        key = torch.nan_to_num(cache.clone(), nan=-float("inf"))
+        if r:
+            key[self.selected[:r]] = -float("inf")
+        self.step(lazy=True)
+        order = torch.sort(key, descending=True, stable=True).indices[: int(self.evals[r])]
+        for c, d in zip(order.cpu().numpy(), cache[order].cpu().numpy()):
+            trace.append((int(c), float(d)))
+        trace.append(("select", int(self.selected[r])))
+
     def result(self):
         """Selections (host list of np.int64), their deltas, and per-round evaluation counts."""
         self.check()
@@ -104,36 +125,76 @@ class GreedyPlacement:
 # Sigma + eps I with a relative eps and takes denom = 1 / P_yy - eps (vgposp_greedy_init_ex's
 # jitter), so a candidate in the span of the others gets denom ~ 0 -> delta 0 at the 1e-8
 # threshold, as with pinv, and every other delta moves by O(eps).
+# A factorization can also "succeed" on a singular cov_vv: a zero pivot that rounds to a tiny
+# positive value.  L^-1 then turns rounding noise into large deltas where pinv gives 0, so a pivot
+# ratio L_ii^2 / sigma_ii below PIVOT_RTOL * n (rounding level) is treated like a failed pivot.
 SINGULAR_EPS = (1e-12, 1e-10, 1e-8)
+PIVOT_RTOL = 100 * np.finfo(np.float64).eps
 
 
-def _place(cov_vv, k, lazy, verbose):
+def _check_pivots(g, sdiag):
+    """After init(): raise CholeskyError if a pivot of Sigma = L L^T is at rounding level.  The
+    factored buffer holds M = L^-1, so L_ii^2 / sigma_ii = 1 / (M_ii^2 sigma_ii)."""
+    g.check()
+    m = torch.diagonal(g.S)
+    ratio = 1.0 / (m * m * sdiag)
+    i = int(torch.argmin(ratio))
+    if not float(ratio[i]) >= PIVOT_RTOL * g.n:
+        raise CholeskyError(i + 1)
+
+
+def _rounds(g, k, lazy, trace):
+    for _ in range(k):
+        if trace is not None:
+            g.step_traced(trace)
+        else:
+            g.step(lazy)
+    return g.result()[0]
+
+
+def _place(cov_vv, k, lazy, verbose, trace=None):
     if k < 1:
         return []
+    if verbose and trace is None:
+        trace = []
+    tr = None if trace is None else []
     try:
-        g = GreedyPlacement(cov_vv, k, copy=True).run(k, lazy=lazy)
-        A, deltas, _ = g.result()
+        g = GreedyPlacement(cov_vv, k, copy=True)
+        sdiag = torch.diagonal(g.S).clone()
+        g.init()
+        _check_pivots(g, sdiag)
+        A = _rounds(g, k, lazy, tr)
     except CholeskyError as err:
         S = linalg.as_device(cov_vv)
         scale = float(torch.mean(torch.diagonal(S)).abs()) or 1.0
         for rel in SINGULAR_EPS:
             try:
-                g = GreedyPlacement(S, k, copy=True, jitter=rel * scale).run(k, lazy=lazy)
-                A, deltas, _ = g.result()
+                tr = None if trace is None else []
+                g = GreedyPlacement(S, k, copy=True, jitter=rel * scale).init()
+                A = _rounds(g, k, lazy, tr)
                 break
             except CholeskyError:
                 continue
         else:
             raise err
-    if verbose:
-        for y, d in zip(A, deltas):
-            print("y*=", y, "delta=", d)
+    if trace is not None:
+        trace.extend(tr)
+    if verbose:  # the reference's lines, placement_algorithm2.py:205 and :188
+        for t in trace:
+            if t[0] == "select":
+                print("y*=", t[1])
+            else:
+                print("delta_y=", t[1], "y_st=", t[0])
     return A
 
 
-def placement_algorithm_2(cov_vv, k, verbose=False):
-    """Lazy greedy MI placement (placement_algorithm2.py:151-219).  Returns k indices."""
-    return _place(cov_vv, k, True, verbose)
+def placement_algorithm_2(cov_vv, k, verbose=False, trace=None):
+    """Lazy greedy MI placement (placement_algorithm2.py:151-219).  Returns k indices.
+
+    ``verbose=True`` prints the reference's per-evaluation lines (``delta_y= … y_st= …`` for every
+    delta evaluated, ``y*= …`` per selection, :205 / :188); ``trace`` (a list) receives the same
+    records as ``(y, delta)`` / ``('select', y)`` tuples without printing."""
+    return _place(cov_vv, k, True, verbose, trace)
 
 
 def placement_algorithm_1(cov_vv, k, verbose=False):

@@ -112,10 +112,12 @@ class ShardedGreedyPlacement:
             if r != self.rank and e > a:
                 d[a:e].copy_(self.recv[r * self.S:r * self.S + (e - a)])
 
-    def _allreduce_piv(self):
+    def _allreduce_piv(self, rnd):
+        """Sum the pivot data of round ``rnd`` (nom, P_yy, W[0..rnd)[y], V[0..rnd)[y]: the
+        2 + 2 rnd entries greedy_select_kernel rewrites; only the owner of y writes non-zeros)."""
         if self.world == 1:
             return
-        p = self.b.piv()
+        p = self.b.piv()[: 2 + 2 * rnd]
         if self.staging:
             h = p.cpu()
             dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
@@ -129,7 +131,7 @@ class ShardedGreedyPlacement:
             self.b.update(rnd, self.c0, self.c1)
             self._allgather_delta()
             self.b.select(rnd, lazy, self.c0, self.c1)
-            self._allreduce_piv()
+            self._allreduce_piv(rnd)
         return self.b.result()
 
 
