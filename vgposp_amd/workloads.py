@@ -55,6 +55,13 @@ def c2_data(n=32, half=2.0):
     return X, 2.0 * grid_spacing(shape)
 
 
+def c4_grid(n=128, seed=0):
+    """Config C4: the 128^3 jittered grid (N = 2,097,152) of the local-kernel greedy, EQ amp 1,
+    ls = 2h -> (X, shape, ls)."""
+    shape = (n, n, n)
+    return grid_points(shape, jitter=0.05, seed=seed), shape, 2.0 * grid_spacing(shape)
+
+
 def vgp_c3_graph(X, y, Z, B, lr=0.01):
     """The reference's training graph (variational_Gaussian_process_example.py:51-102) in this
     package's API -> (train_op, loss, x_batch placeholder, y_batch placeholder)."""
