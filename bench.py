@@ -2,19 +2,21 @@
 (64 x 32 x 32, EQ kernel) — BASELINE.json's metric "greedy sensor placements/sec + fp64 Cholesky
 GF/s on N=65k 3D grid".
 
-One step = the whole job for one spatial split, with the grid points already resident in HBM:
+One step = the whole job for ONE placement problem, with the grid points already resident in HBM:
   assemble Sigma = K(X, X) + (noise + jitter) I  (kernel_matrix, HBM-write-bound)
   -> fused Cholesky + inverse of Sigma             (potrf sweep, fp64 MFMA-bound, 2N^3/3 flops)
   -> k = 50 lazy-greedy selections                 (per round one HBM-bound triangular mat-vec)
-value = placements per second of the whole job (all ranks).  With --gpus N every rank owns one
-64x32x32 split of a (64 N) x 32 x 32 domain (the reference splits its domain the same way,
-main_architecture_2_sampledistribution.py:987-989), so per-GPU work is fixed: weak scaling, no
-collective in the data path (only the timing barrier / max-reduction).
+value = placements per second of that job.  With --gpus N the SAME problem is candidate-sharded
+over the N ranks (vgposp_amd.sharded_placement over RCCL: per round one all-gather of the delta
+slabs and one pivot all-reduce); the O(N^3) factorization is replicated on every rank (SURVEY
+§8(e): "Cholesky at N <= 65k: replicas only"), so this is strong scaling whose speed-up that
+replicated init bounds (DESIGN.md §6).  The timed loop runs with the library's event timing OFF;
+the roofline numbers come from one more, profiled, step.
 
-Also reported: fp64 Cholesky GF/s (plain potrf of the same Sigma, N^3/3 flops), the roofline of
-the dominant kernel measured live with the library's HIP-event profiling, and a CPU baseline
-(the oracle's pinv-faithful restatement of placement_algorithm2.py timed on the host cores on a
-bounded sample).
+Also reported: fp64 Cholesky GF/s (plain potrf of the same Sigma, N^3/3 flops); config C4 (the
+128^3 local-kernel greedy, candidates sharded over the same ranks: where sharding pays); at N > 1
+the independent-splits throughput (one 64x32x32 split per rank) as a labelled extra; at N = 1 the
+C2 / C3 / C5 lines and a CPU baseline (the oracle timed on the host cores).
 """
 from __future__ import annotations
 
@@ -50,6 +52,10 @@ def parse():
     p.add_argument("--no-vgp", action="store_true", help="skip the C3 / C5 VGP training lines")
     p.add_argument("--no-c2", action="store_true", help="skip the C2 assembly + potrf line")
     p.add_argument("--vgp-steps", type=int, default=10)
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 local greedy) line")
+    p.add_argument("--c4-steps", type=int, default=10)
+    p.add_argument("--no-splits", action="store_true",
+                   help="skip the N > 1 independent-splits extra")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r1.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
@@ -78,43 +84,57 @@ def cpu_model():
 
 
 def cpu_baseline(args, N):
-    """Oracle restatement of placement_algorithm2.placement_algorithm_2 (pinv per candidate, the
-    reference's algorithm) timed on the host on a bounded sample, plus OpenBLAS Cholesky GF/s."""
+    """The same algorithm on the host: the oracle's incremental-precision lazy greedy
+    (oracle.placement.placement_lazy_incremental: LAPACK dpotrf + dpotri once, O(N^2) numpy per
+    round — the maths the HIP path runs) on a jittered 16x16x32 grid (N = 8,192), k = 50, all BLAS
+    threads; plus the reference's own algorithm (the pinv-faithful restatement of
+    placement_algorithm2.py, one SVD per delta evaluation) on an 8^3 grid with k = 2, and an
+    OpenBLAS Cholesky of the same kernel family."""
     from oracle import gp as ogp
     from oracle import placement as op
     from vgposp_amd.data_generation import grid_points, grid_spacing
 
-    shape = tuple(args.cpu_shape)
-    X = grid_points(shape, jitter=0.05, seed=0)
-    h = grid_spacing(shape)
-    S = ogp.kernel_matrix(args.kernel, X, X, 1.0, 2 * h)[0] + (args.noise + 1e-6) * np.eye(len(X))
+    def sigma(shape):
+        X = grid_points(shape, jitter=0.05, seed=0)
+        S = ogp.kernel_matrix(args.kernel, X, X, 1.0, 2 * grid_spacing(shape))[0]
+        S[np.diag_indices(len(X))] += args.noise + 1e-6
+        return S
+
+    shape = (16, 16, 32)
+    S = sigma(shape)
+    t0 = time.perf_counter()
+    op.placement_lazy_incremental(S, args.k)
+    t_inc = time.perf_counter() - t0
+    del S
+    ps = tuple(args.cpu_shape)
+    Sp = sigma(ps)
     trace = []
     t0 = time.perf_counter()
-    op.placement_algorithm_2(S, args.cpu_k, trace=trace)
-    t = time.perf_counter() - t0
+    op.placement_algorithm_2(Sp, args.cpu_k, trace=trace)
+    t_pinv = time.perf_counter() - t0
     nevals = sum(1 for e in trace if e[0] != "select")
-    n_s = len(X)
-    t_eval = t / max(nevals, 1)
-    # round 1 alone needs N evaluations of an O(N^3) pinv: a lower bound on the time at N
-    t_lb = t_eval * (N / n_s) ** 3 * N
-    # OpenBLAS Cholesky of the same kernel family at a bounded size
     nc = 6144
-    Xc = grid_points((24, 16, 16), jitter=0.0)
-    Sc = ogp.kernel_matrix(args.kernel, Xc, Xc, 1.0, 2 * grid_spacing((24, 16, 16)))[0]
-    Sc[np.diag_indices(nc)] += args.noise + 1e-6
+    Sc = sigma((24, 16, 16))
     t0 = time.perf_counter()
     np.linalg.cholesky(Sc)
     tc = time.perf_counter() - t0
+    n_inc = int(np.prod(shape))
     return {
-        "value": args.cpu_k / t,
+        "value": args.k / t_inc,
         "unit": "placements/s",
         "cores": cpu_threads(),
         "kind": "port",
-        "sample": (f"oracle pinv restatement of placement_algorithm_2 on a jittered "
-                   f"{shape[0]}x{shape[1]}x{shape[2]} grid (N={n_s}), k={args.cpu_k}: {nevals} "
-                   f"delta evaluations in {t:.1f} s; numpy/OpenBLAS cholesky at N={nc}"),
-        "extrapolated_value_at_N": args.k / t_lb,
+        "sample": (f"oracle placement_lazy_incremental (same algorithm as the GPU path) on a "
+                   f"jittered {shape[0]}x{shape[1]}x{shape[2]} grid (N={n_inc}), k={args.k}: "
+                   f"{t_inc:.1f} s; the GPU line is at N={N}, where the O(N^3) init alone is "
+                   f"{(N / n_inc) ** 3:.0f}x this sample's"),
+        "reference_algorithm": {
+            "value": args.cpu_k / t_pinv, "unit": "placements/s",
+            "sample": (f"pinv restatement of placement_algorithm2.placement_algorithm_2 on a "
+                       f"jittered {ps[0]}x{ps[1]}x{ps[2]} grid (N={len(Sp)}), k={args.cpu_k}: "
+                       f"{nevals} delta evaluations (one SVD each) in {t_pinv:.1f} s")},
         "cholesky_gflops": nc ** 3 / 3 / tc / 1e9,
+        "cholesky_sample": f"numpy.linalg.cholesky at N={nc}",
         "cpu_model": cpu_model(),
     }
 
@@ -223,6 +243,85 @@ def c2_line(reps=2):
             "potrf_ms": t_c * 1e3, "potrf_gflops": n ** 3 / 3.0 / t_c / 1e9}
 
 
+def c4_line(args, world, rank, barrier, maxtime):
+    """Config C4: 128^3 = 2,097,152 candidates, k = 50, the local-kernel greedy
+    (algorithm 3 with epsilon-local deltas on the beta = 4 taper, window cutoff 3), candidates
+    sharded over the ranks by i0-planes with one 16-byte key all-gather per pick."""
+    import torch
+
+    from vgposp_amd import _lib
+    from vgposp_amd.local_placement import HipLocalBackend, LocalGreedyPlacement, plane_slabs
+    from vgposp_amd.workloads import c4_grid
+    X, shape, ls = c4_grid()
+    c0, c1 = plane_slabs(shape, world)[rank]
+    k, beta, cutoff = args.k, 4.0, 3
+    b = HipLocalBackend(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6, c0=c0,
+                        c1=c1)
+    g = LocalGreedyPlacement(b)
+    for _ in range(2):
+        g.run(k)
+    reps = args.c4_steps
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.run(k)
+    torch.cuda.synchronize()
+    barrier()
+    dt = maxtime(time.perf_counter() - t0) / reps
+    b.check()
+    _lib.prof_enable(True)
+    g.run(k)
+    prof = _lib.prof_dump()
+    _lib.prof_enable(False)
+    out = {"metric": "greedy sensor placements/sec", "value": k / dt, "unit": "placements/s",
+           "ms_per_step": dt * 1e3, "n_gpus": world, "scaling": "strong",
+           "config": {"workload": "C4: 128^3 jittered grid (N=2,097,152), EQ amp 1 ls 2h, "
+                                  f"noise {args.noise}+1e-6, beta-decay taper beta={beta} "
+                                  f"(support {b.m} points), window cutoff {cutoff}, k={k}, "
+                                  "local-kernel algorithm 3",
+                      "N": int(np.prod(shape)), "k": k, "parallelism": f"candidates{world}"},
+           "picks_head": [int(v) for v in b.picks[:6].cpu()],
+           "breakdown_ms": {n: v[0] for n, v in prof.items()},
+           "note": ("latency-bound: per pick an arg-max, a 216-candidate window re-score and (N > 1) "
+                    "one key all-gather; round 0 scores every candidate once")}
+    return out
+
+
+def splits_line(args, world, barrier, maxtime, rank):
+    """N > 1 extra: one independent 64x32x32 split per rank (weak scaling, no collective)."""
+    import torch
+
+    from vgposp_amd import linalg
+    from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    from vgposp_amd.workloads import placement_split
+    X, ls = placement_split(tuple(args.shape), rank)
+    N = len(X)
+    Xd = linalg.as_device(X)
+    Sigma = torch.empty((N, N), dtype=torch.float64, device="cuda")
+    g = GreedyPlacement(Sigma, args.k)
+
+    def step():
+        linalg.kernel_matrix(args.kernel, Xd, None, 1.0, ls, diag_shift=args.noise + 1e-6,
+                             out=Sigma[None])
+        g.run(args.k)
+
+    step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = maxtime(time.perf_counter() - t0)
+    del Sigma, g
+    torch.cuda.empty_cache()
+    return {"metric": "greedy sensor placements/sec (independent splits)",
+            "value": world * args.k / dt, "unit": "placements/s", "scaling": "weak",
+            "config": {"workload": f"one jittered {args.shape} split per rank (seed = rank), "
+                                   "dense-exact, no collective", "splits": world}}
+
+
 def main():
     args = parse()
     import torch
@@ -239,12 +338,24 @@ def main():
 
     from vgposp_amd import _lib, linalg
     from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    from vgposp_amd.sharded_placement import HipGreedyBackend, ShardedGreedyPlacement
     from vgposp_amd.workloads import placement_split
 
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def maxtime(t):
+        if world == 1:
+            return t
+        v = torch.tensor([t], dtype=torch.float64, device="cuda")
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        return float(v.item())
+
     shape = tuple(args.shape)
-    # jittered grid (seed = rank) so the selections are decided by the data, not by the exact
-    # octant ties of a regular grid; this rank's split is shifted along axis 0
-    X, ls = placement_split(shape, rank)
+    # ONE problem on every rank: a jittered grid (seed 0) so the selections are decided by the
+    # data, not by the exact octant ties of a regular grid
+    X, ls = placement_split(shape, 0)
     N = X.shape[0]
     k = args.k
     Xd = linalg.as_device(X)
@@ -252,25 +363,32 @@ def main():
     ls_d = linalg.as_device([ls])
     shift_d = linalg.as_device([args.noise + 1e-6])
     Sigma = torch.empty((N, N), dtype=torch.float64, device="cuda")
-    g = GreedyPlacement(Sigma, k)  # Sigma is factored in place every step
+    if world == 1:
+        g = GreedyPlacement(Sigma, k)  # Sigma is factored in place every step
+
+        def run_rounds():
+            g.init()
+            for _ in range(k):
+                g.step(lazy=True)
+        selected = g.selected
+    else:
+        sh = ShardedGreedyPlacement(HipGreedyBackend(Sigma, k))
+        g = sh.b.g
+
+        def run_rounds():
+            sh.run(k)
+        selected = g.selected
 
     def step():
         linalg.kernel_matrix(args.kernel, Xd, None, amp_d, ls_d, diag_shift=shift_d, out=Sigma[None])
-        g.init()
-        for _ in range(k):
-            g.step(lazy=True)
+        run_rounds()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     g.check()
-    ref_sel = g.selected.clone()
+    ref_sel = selected.clone()
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    _lib.prof_enable(True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -278,23 +396,25 @@ def main():
         step()
     torch.cuda.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = maxtime(time.perf_counter() - t0)
+    g.check()
+    deterministic = bool(torch.equal(ref_sel, selected))
+
+    # one more step with the library's per-launch event timing on: the roofline numbers
+    _lib.prof_enable(True)
+    step()
+    torch.cuda.synchronize()
     prof = {name: _lib.prof_query(name) for name in
             ["kernel_matrix", "gemm_f64", "potrf_diag", "greedy_colsq", "greedy_trmv", "greedy_update"]}
-    # exact algorithmic bytes of the triangular mat-vec: rows >= a of the lower triangle of L^-1
-    # (the library only knows the full-triangle upper bound at launch time; a lives on device)
-    sel = [int(v) for v in g.selected.cpu()]
-    tri = lambda x: x * (x + 1) / 2.0  # noqa: E731
-    trmv_bytes = 8.0 * sum(tri(N) - tri(a) + 2 * N for a in sel[:-1]) * args.steps
-    ms_t, n_t, _, _ = prof["greedy_trmv"]
-    prof["greedy_trmv"] = (ms_t, n_t, 0.0, trmv_bytes)
     _lib.prof_enable(False)
-    g.check()
-    deterministic = bool(torch.equal(ref_sel, g.selected))
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # exact algorithmic bytes of the triangular mat-vec: rows >= a of the lower triangle of L^-1
+    # over this rank's candidate columns (the library only knows the full-triangle upper bound at
+    # launch time; a lives on device)
+    sel = [int(v) for v in selected.cpu()]
+    tri = lambda x: x * (x + 1) / 2.0  # noqa: E731
+    trmv_bytes = 8.0 * sum(tri(N) - tri(a) + 2 * N for a in sel[:-1])
+    ms_t, n_t, _, _ = prof["greedy_trmv"]
+    prof["greedy_trmv"] = (ms_t, n_t, 0.0, trmv_bytes if world == 1 else 0.0)
 
     # separate plain potrf (N^3/3) for the Cholesky GF/s figure
     chol_gflops = None
@@ -307,6 +427,12 @@ def main():
         ev1.record()
         torch.cuda.synchronize()
         chol_gflops = N ** 3 / 3 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+    del Sigma
+    torch.cuda.empty_cache()
+
+    c4 = None if args.no_c4 else c4_line(args, world, rank, barrier, maxtime)
+    splits = splits_line(args, world, barrier, maxtime, rank) if world > 1 and not args.no_splits \
+        else None
 
     if rank != 0:
         if world > 1:
@@ -314,8 +440,8 @@ def main():
         return
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * k * args.steps / elapsed
-    # dominant kernel by time over the timed region
+    value = k * args.steps / elapsed
+    # dominant kernel by time in the profiled step
     dom = max(prof, key=lambda n: prof[n][0])
     ms, launches, flops, nbytes = prof[dom]
     if flops > 0 and dom == "gemm_f64":
@@ -327,7 +453,9 @@ def main():
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None}
     roof.update({"kernel": dom, "launches": launches, "avg_launch_ms": ms / max(launches, 1),
-                 "share_of_step": ms / (elapsed * 1e3)})
+                 "share_of_step": ms / ms_per_step,
+                 "measured": "HIP events around every launch on the library's stream, in one extra "
+                             "profiled step after the timed loop"})
     tr = load_traffic(args.traffic, dom, N, shape, k)
     if tr is not None:
         roof["traffic"] = tr["bytes_per_launch"]
@@ -339,16 +467,16 @@ def main():
     # the HBM-bound kernel of the placement rounds, with its PMC-measured traffic
     ms_t, n_t, _, by_t = prof["greedy_trmv"]
     hbm = {"kernel": "greedy_trmv", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-           "achieved": by_t / (ms_t * 1e-3) / 1e9 if ms_t else None, "launches": n_t,
+           "achieved": by_t / (ms_t * 1e-3) / 1e9 if ms_t and by_t else None, "launches": n_t,
            "avg_launch_ms": ms_t / max(n_t, 1), "traffic": None}
     if hbm["achieved"] is not None:
         hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
     trm = load_traffic(args.traffic, "greedy_trmv", N, shape, k)
-    if trm is not None and n_t:
+    if trm is not None and n_t and by_t:
         hbm["traffic"] = trm["bytes_per_launch"]
         hbm["traffic_vs_algorithmic"] = trm["bytes_per_launch"] / (by_t / n_t)
         hbm["traffic_source"] = trm["source"]
-    breakdown = {n: {"ms_per_step": v[0] / args.steps, "launches_per_step": v[1] / args.steps,
+    breakdown = {n: {"ms_per_step": v[0], "launches_per_step": v[1],
                      "achieved": (v[2] / (v[0] * 1e-3) / 1e12 if v[2] and n == "gemm_f64" else
                                   v[3] / max(v[0], 1e-9) / 1e6),
                      "unit": "TFLOP/s" if n == "gemm_f64" else "GB/s"}
@@ -362,21 +490,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": f"{shape[0]}x{shape[1]}x{shape[2]} grid per split (N={N}), "
+        "config": {"workload": f"{shape[0]}x{shape[1]}x{shape[2]} jittered grid (N={N}), "
                                f"{args.kernel.upper()} kernel amp=1 ls=2h noise={args.noise}+1e-6, "
-                               f"k={k} lazy-greedy MI placements, dense-exact",
-                   "N": N, "k": k, "splits": world, "parallelism": f"split{world}"},
+                               f"k={k} lazy-greedy MI placements, dense-exact, one problem"
+                               + (f" candidate-sharded over {world} ranks (RCCL), factorization "
+                                  "replicated" if world > 1 else ""),
+                   "N": N, "k": k, "parallelism": f"candidates{world}" if world > 1 else "single",
+                   "rccl_world_size": world if world > 1 else None},
         "cholesky_gflops": chol_gflops,
         "roofline": roof,
         "roofline_hbm": hbm,
         "breakdown": breakdown,
         "deterministic_selection": deterministic,
-        "selected_head": [int(a) for a in g.selected[:8].cpu()],
+        "selected_head": sel[:8],
     }
+    if c4 is not None:
+        out["c4"] = c4
+    if splits is not None:
+        out["independent_splits"] = splits
     if world == 1 and not args.no_vgp:
         out["vgp_c3"] = vgp_line(args, "c3")
         out["vgp_c5"] = vgp_line(args, "c5")
