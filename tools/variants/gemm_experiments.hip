@@ -1,3 +1,12 @@
+// EXPERIMENT SOURCE — not part of libvgposp.so.  The product GEMM is vgposp_amd/csrc/gemm.hip.
+// This is the round-1 gemm.hip with every measured-and-rejected variant still in it:
+// the one-wave-per-SIMD register-staged kernel gemm_rs_kernel (VGPOSP_GEMM_RS=1/2), the 256x128
+// configurations (VGPOSP_GEMM_CFG=2/3), b128 fragment reads (-DVGPOSP_GEMM_B128=1), per-cluster
+// s_setprio (-DVGPOSP_GEMM_EXP_PRIO, VGPOSP_GEMM_PRIO), the timing-only builds that give wrong
+// results (-DVGPOSP_GEMM_EXP_NOVMWAIT / _NOBARRIER / _NOLOADS) and the reference-kernel switch
+// (VGPOSP_GEMM_REF=1).  tools/build_variant.sh compiles it in place of gemm.hip into
+// tools/variants/lib_NAME.so (loaded with VGPOSP_LIB=...) so the A/B scripts keep reproducing the
+// numbers DESIGN.md quotes.  It includes the library's headers from vgposp_amd/csrc.
 // fp64 GEMM on CDNA4 matrix cores (v_mfma_f64_16x16x4f64), the dense contraction behind the
 // Cholesky trailing update, the fused block Gauss-Jordan inverse and C^-1 = M^T M formation.
 //
@@ -18,7 +27,7 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "common.h"
+#include "../../vgposp_amd/csrc/common.h"
 
 namespace vgposp {
 
@@ -48,6 +57,7 @@ struct GemmParams {
   int nsplit, nblk;
   int64_t kchunk;
   double* part;
+  int prio;  // experiment (VGPOSP_GEMM_PRIO): 1 = s_setprio 1 for the second wave of each SIMD pair
 };
 
 // Stage one operand tile (128 rows of the M/N dimension x 16 of K) into registers.
@@ -283,16 +293,18 @@ __device__ __forceinline__ int tri_root(int64_t id) {
   return (int)t;
 }
 
-// Tile configuration: 128x128 tiles, 4 waves of 64x64 (4x4 fragments), a STAGES-deep ring, 2
-// workgroups per CU.  (The 256x128 configurations measured against it live in
-// tools/variants/gemm_experiments.hip.)
+// CFG selects the tile shape (waves always in a (rows / 64 or 128) x 2 grid over the tile):
+//   1 -> 128x128 tiles, 4 waves of 64x64 (4x4 fragments), STAGES-deep ring, 2 workgroups per CU;
+//   2 -> 256x128 tiles, 4 waves of 128x64 (8x4 fragments, 128 accumulators in AGPRs), 3-stage
+//        ring (144 KiB), 1 workgroup per CU;
+//   3 -> 256x128 tiles, 8 waves of 64x64, 3-stage ring, 1 workgroup per CU: two waves per SIMD
+//        as in 1, but 6 instead of 8 LDS-DMA pieces per wave per 64 MFMAs and a deeper ring.
 template <int CFG> struct GemmCfg {
-  static_assert(CFG == 1, "only the 128x128 configuration is built into the library");
-  static constexpr int NSUB = 1;              // 128-row A sub-tiles
-  static constexpr int NW = 4;                // waves
-  static constexpr int FI = 4;                // 16-row fragments per wave
-  static constexpr int NST = STAGES;          // ring depth
-  static constexpr int OCC = VGPOSP_GEMM_OCC;  // workgroups per CU (launch bound)
+  static constexpr int NSUB = CFG == 1 ? 1 : 2;              // 128-row A sub-tiles
+  static constexpr int NW = CFG == 3 ? 8 : 4;                // waves
+  static constexpr int FI = CFG == 2 ? 8 : 4;                // 16-row fragments per wave
+  static constexpr int NST = CFG == 1 ? STAGES : 3;          // ring depth
+  static constexpr int OCC = CFG == 1 ? VGPOSP_GEMM_OCC : 1;  // workgroups per CU (launch bound)
 };
 
 template <bool TA, bool TB, bool TRIA, bool TRIB, int CFG>
@@ -308,7 +320,15 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   constexpr int PO = 16 / NW;                          // pieces per operand per wave
   constexpr int PPW = PO * (NSUB + 1);                 // pieces per wave per stage (8, 12 or 6)
   constexpr bool SPREAD = NST >= 3;                    // next-tile loads between the MFMAs
-  constexpr bool A_IL = false, B_IL = false;  // plain fragment order
+#if VGPOSP_GEMM_B128
+  // b128 fragment reads (experiment): lane group fk covers k = 4 fk + s (s = 0..3), so a KC
+  // operand's substeps 2h and 2h + 1 are one 16-byte pair; an MC operand's 16-byte pair is two
+  // adjacent rows of one k, i.e. fragments 2g and 2g + 1 (rows 32 g + 2 x + {0, 1}).
+  constexpr bool B128 = NST == 2;
+#else
+  constexpr bool B128 = false;
+#endif
+  constexpr bool A_IL = B128 && !A_KC, B_IL = B128 && !B_KC;  // row-interleaved fragments
   __shared__ __attribute__((aligned(16))) double smem[NST * SE];
 
   // Tile order.  Uniform-K launches: XCD-aware bijective remap (each XCD walks a contiguous range
@@ -346,6 +366,7 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fk = lane >> 4;
+  if (p.prio == 1 && (NW == 8 ? wave >= 4 : (bid >> 3) & 1)) __builtin_amdgcn_s_setprio(1);
 
   // K range that can contribute when an operand is stored lower triangular.
   int64_t kbeg = 0, kend = p.k;
@@ -396,7 +417,11 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   for (int t = 0; t < T; ++t) {
     const int after = min(T - 1 - t, NST - 2);  // tiles that may stay in flight
     static_assert(PPW == 8 || PPW == 12 || PPW == 6, "counted waits: 6, 8 or 12 pieces");
+#ifdef VGPOSP_GEMM_EXP_NOVMWAIT  // timing experiment only: results are wrong
+    if (false) {
+#else
     if (after == 0) {
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (PPW == 8) {
       if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -409,11 +434,17 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
       else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef VGPOSP_GEMM_EXP_NOBARRIER  // timing experiment only: results are wrong
     __builtin_amdgcn_s_barrier();
+#endif
     // 3-stage ring: the next K-tile's pieces are spread over the k-slices below, between MFMAs
     // (issued back to back they park the wave for their issue cost; 8192^3 NT 63.3 -> 65.7 TF/s).
     // 2-stage ring: issued here, as early as possible — the tile is needed one K-step later.
+#ifdef VGPOSP_GEMM_EXP_NOLOADS  // timing experiment only: no loads after the prologue
+    const bool more = false;
+#else
     const bool more = t + NST - 1 < T;
+#endif
     if (!SPREAD && more) issue(t + NST - 1);
 
     const double* As = smem + (t % NST) * SE + ((wm * WROWS) / GBM) * OPND_ELEMS;
@@ -423,6 +454,68 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     // of a triangular operand (k0 within 128 of the tile's first row / column)
     const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + TBM && k0 + GBK > m0) ||
                       (TRIB && k0 < n0 + GBN && k0 + GBK > n0);
+    if constexpr (B128) {
+      // x[e][f]: substep 2h + e of fragment f; rb = the wave's first row of the operand image
+      auto frags = [&](auto kc, const double* X, int rb, auto nf, int h, double (&x)[2][decltype(nf)::value]) {
+        constexpr int F = decltype(nf)::value;
+        if constexpr (decltype(kc)::value) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            const int r = rb + f * 16 + fr;
+            const double2 v = *reinterpret_cast<const double2*>(X + r * 16 + 2 * ((2 * fk + h) ^ ((r & 15) >> 1)));
+            x[0][f] = v.x;
+            x[1][f] = v.y;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int k = 4 * fk + 2 * h + e;
+#pragma unroll
+            for (int g = 0; g < F / 2; ++g) {
+              const int pr = (rb >> 1) + 16 * g + fr;
+              const double2 v = *reinterpret_cast<const double2*>(X + k * 128 + 2 * (pr ^ ((k & 1) << 3)));
+              x[e][2 * g] = v.x;
+              x[e][2 * g + 1] = v.y;
+            }
+          }
+        }
+      };
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        double a[2][FI], b[2][4];
+        frags(std::integral_constant<bool, A_KC>{}, As, (wm * WROWS) % GBM, std::integral_constant<int, FI>{}, h, a);
+        frags(std::integral_constant<bool, B_KC>{}, Bs, wn * 64, std::integral_constant<int, 4>{}, h, b);
+        if (mask) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int64_t gk = k0 + 4 * fk + 2 * h + e;
+#pragma unroll
+            for (int i = 0; i < FI; ++i) {
+              const int64_t gm = m0 + wm * WROWS + (A_IL ? 32 * (i >> 1) + 2 * fr + (i & 1) : i * 16 + fr);
+              if (gk >= kend || (TRIA && (TA ? gm > gk : gk > gm))) a[e][i] = 0.0;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int64_t gn = n0 + wn * 64 + (B_IL ? 32 * (j >> 1) + 2 * fr + (j & 1) : j * 16 + fr);
+              if (gk >= kend || (TRIB && (TB ? gk > gn : gn > gk))) b[e][j] = 0.0;
+            }
+          }
+        }
+#ifdef VGPOSP_GEMM_EXP_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int i = 0; i < FI; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[e][i], b[e][j], acc[i][j], 0, 0, 0);
+#ifdef VGPOSP_GEMM_EXP_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      }
+    } else
 #pragma unroll
     for (int ks = 0; ks < GBK / 4; ++ks) {
       const int k = ks * 4 + fk;
@@ -454,11 +547,17 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
 #pragma unroll
         for (int q = (ks * PPW) / 4; q < ((ks + 1) * PPW) / 4; ++q) issue_piece(t + NST - 1, q);
       }
+#ifdef VGPOSP_GEMM_EXP_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+#ifdef VGPOSP_GEMM_EXP_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
   }
 
@@ -487,6 +586,385 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// "rs" path: one wave per SIMD, register-staged operands, 128x256 (FM = 4, FN = 8) or 256x128
+// (FM = 8, FN = 4) tiles.  Each wave owns a (16 FM) x (16 FN) block of C: FM * FN = 32 f64 MFMA
+// accumulators (256 registers, AGPRs), so one K-substep is 32 MFMAs (~2k cycles) against 6 LDS
+// reads.  Per K-tile (16 deep) every thread issues FM + FN 16-byte global loads for the tile
+// after next into registers, and writes the tile after this one from those registers to the other
+// LDS buffer (one barrier per K-tile).  Zero-masking of triangular operands and of the K tail is
+// applied in registers between the load and the LDS write, so the MFMA loop has no branches.
+//
+// LDS images (both read with ds_read_b128, both conflict-free for the b128 lane groups):
+//   KC operand (stored [row][k]):  row-major [rows][16 k]; 16-byte pair P of row r at slot
+//       P ^ ((r >> 1) & 5).  Lane (fr, fk) reads pair 2 fk + h: k = 4 fk + 2h, 4 fk + 2h + 1,
+//       i.e. substeps 2h and 2h + 1 of k-map  k(s, fk) = 4 fk + s.
+//   MC operand (stored [k][row]):  [16 k][rows]; lane (fr, fk) of substep s reads rows
+//       32 g + 2 fr, 32 g + 2 fr + 1 of k-row 4 fk + s: fragment 2g holds the even rows and
+//       fragment 2g + 1 the odd ones (the epilogue undoes the interleave).
+// ---------------------------------------------------------------------------------------------
+// sched_group_barrier patterns of gemm_rs_kernel (masks: 0x2 VALU, 0x8 MFMA, 0x20 VMEM read,
+// 0x100 DS read, 0x200 DS write)
+template <int R>
+__device__ __forceinline__ void sgb_reads() {
+  if constexpr (R > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    sgb_reads<R - 1>();
+  }
+}
+// MG MFMAs carrying one staged piece (mask VALU, LDS write, buffer load) and RD fragment reads
+template <int MG, int RD>
+__device__ __forceinline__ void sgb_group() {
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+  sgb_reads<RD>();
+  if constexpr (MG - 4 - RD > 0) __builtin_amdgcn_sched_group_barrier(0x008, MG - 4 - RD, 0);
+}
+// after the barrier: RD reads under NM MFMAs
+template <int RD, int NM>
+__device__ __forceinline__ void sgb_tail() {
+  if constexpr (RD > 0 && NM > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    sgb_tail<RD - 1, NM - 1>();
+  } else if constexpr (RD > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+  } else if constexpr (NM > 0) {
+    __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+  }
+}
+
+__device__ double g_rs_sink[64];  // dropped epilogue stores of gemm_rs_kernel
+
+template <bool KC>
+__device__ __forceinline__ int rs_row(int f, int x) {  // operand row of fragment f, lane index x
+  return KC ? 16 * f + x : 32 * (f >> 1) + 2 * x + (f & 1);
+}
+
+template <int FM, int FN, bool TA, bool TB, bool TRIA, bool TRIB>
+__global__ __launch_bounds__(256, 1) void gemm_rs_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int BM = 32 * FM, BN = 32 * FN;
+  constexpr bool A_KC = !TA, B_KC = TB;
+  constexpr int AE = BM * 16, BE = BN * 16;  // doubles per operand per stage
+  constexpr int SE = AE + BE;
+  __shared__ __attribute__((aligned(16))) double smem[2 * SE];
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  int wg = bid;
+  if (!TRIA) {
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  }
+  int zsplit = 0;
+  if (p.nsplit > 1) {
+    zsplit = wg / p.nblk;
+    wg -= zsplit * p.nblk;
+  }
+  int ti, tj;
+  if (p.uplo_c == VGPOSP_LOWER) {
+    // tiles on or below the diagonal, row by row: row ti holds c(ti) = (BM ti + BM - 1) / BN + 1
+    // column tiles; with BM = 2 BN that is 2 ti + 2 (cumulative ti (ti + 1)), with BN = 2 BM it
+    // is ti / 2 + 1 (cumulative over row pairs u: u (u + 1))
+    if (BM >= BN) {
+      ti = tri_root(wg / 2);
+      while ((int64_t)(ti + 1) * (ti + 2) <= wg) ++ti;
+      while ((int64_t)ti * (ti + 1) > wg) --ti;
+      tj = wg - ti * (ti + 1);
+    } else {
+      int u = tri_root(wg / 2);
+      while ((int64_t)(u + 1) * (u + 2) <= wg) ++u;
+      while ((int64_t)u * (u + 1) > wg) --u;
+      const int rem = wg - u * (u + 1);
+      ti = 2 * u + rem / (u + 1);
+      tj = rem % (u + 1);
+    }
+  } else {
+    constexpr int GROUP = 8;
+    const int per_group = GROUP * tiles_n;
+    const int g = wg / per_group, first = g * GROUP;
+    const int gsize = min(GROUP, tiles_m - first);
+    const int local = wg - g * per_group;
+    ti = first + local % gsize;
+    tj = local / gsize;
+    if (TRIA && !TA) ti = tiles_m - 1 - ti;  // longest K ranges first
+  }
+  const int m0 = ti * BM, n0 = tj * BN;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+
+  int64_t kbeg = 0, kend = p.k;
+  if (TRIA) {
+    if (TA) kbeg = max(kbeg, (int64_t)m0);
+    else kend = min(kend, (int64_t)m0 + BM);
+  }
+  if (TRIB) {
+    if (TB) kend = min(kend, (int64_t)n0 + BN);
+    else kbeg = max(kbeg, (int64_t)n0);
+  }
+  if (p.nsplit > 1) {
+    kbeg = max(kbeg, (int64_t)zsplit * p.kchunk);
+    kend = min(kend, (int64_t)(zsplit + 1) * p.kchunk);
+  }
+  kbeg = (kbeg / GBK) * GBK;
+  if (kend < kbeg) kend = kbeg;
+  const int T = (int)((kend - kbeg + GBK - 1) / GBK);
+
+  // ---- staging: FM pieces of A, FN of B per thread (buffer loads, out-of-range reads are 0) ----
+  // piece e = t + 256 q.  KC: row e >> 3, pair e & 7.  MC: k-row e / (rows / 2), pair e % (rows / 2).
+  // Every piece of an operand is the thread's first piece plus q times a fixed stride.  The resource is
+  // rebuilt per K-tile: based at (tile row, k0) and sized to the tile's valid rows (KC) or k-rows
+  // (MC), so rows past the matrix (KC) and the K tail (MC) read as zero.
+  constexpr int AH = BM / 2, BH = BN / 2;  // MC pairs per k-row
+  const int voffA = A_KC ? (int)(((t >> 3) * p.lda + 2 * (t & 7)) * 8)
+                         : (int)(((t / AH) * p.lda + 2 * (t % AH)) * 8);
+  const int voffB = B_KC ? (int)(((t >> 3) * p.ldb + 2 * (t & 7)) * 8)
+                         : (int)(((t / BH) * p.ldb + 2 * (t % BH)) * 8);
+  const int strA = A_KC ? (int)(32 * p.lda * 8) : (int)((256 / AH) * p.lda * 8);
+  const int strB = B_KC ? (int)(32 * p.ldb * 8) : (int)((256 / BH) * p.ldb * 8);
+  // LDS write offsets (doubles) of piece 0; piece q is + 512 q
+  const int lA = A_KC ? (t >> 3) * 16 + 2 * ((t & 7) ^ (((t >> 3) >> 1) & 5)) : (t / AH) * BM + 2 * (t % AH);
+  const int lB = AE + (B_KC ? (t >> 3) * 16 + 2 * ((t & 7) ^ (((t >> 3) >> 1) & 5))
+                            : (t / BH) * BN + 2 * (t % BH));
+  const int K = (int)p.k;
+  const int nrowsA = min(BM, (int)p.m - m0), nrowsB = min(BN, (int)p.n - n0);
+  auto rsrc = [&](bool isA, int tile) {
+    const bool kc = isA ? A_KC : B_KC;
+    const double* X = isA ? p.A : p.B;
+    const int64_t ld = isA ? p.lda : p.ldb;
+    const int r0 = isA ? m0 : n0, nrows = isA ? nrowsA : nrowsB;
+    const int k0 = (int)kbeg + GBK * tile;
+    const double* base;
+    int64_t rec;
+    // the range ends at the last valid element (not at the end of its row: the operand may be
+    // the bottom-right block of a larger matrix, with nothing allocated after it)
+    const int R = (int)(isA ? p.m : p.n);
+    if (kc) {
+      base = X + (int64_t)r0 * ld + min(k0, K);
+      rec = nrows > 0 ? (int64_t)(nrows - 1) * ld + (K - min(k0, K)) : 0;
+    } else {
+      const int kr = min(GBK, K - min(k0, K));
+      base = X + (int64_t)min(k0, K) * ld + r0;
+      rec = kr > 0 ? (int64_t)(kr - 1) * ld + (R - r0) : 0;
+    }
+    // uniform by construction; readfirstlane keeps the resource in SGPRs (a VGPR resource
+    // would turn every load into a waterfall loop)
+    const uint64_t ba = reinterpret_cast<uint64_t>(base);
+    const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ba >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ba);
+    const int nrec = __builtin_amdgcn_readfirstlane((int)max(rec * 8, (int64_t)0));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(bu), (short)0, nrec, 0x00020000);
+  };
+  double2 stg[FM + FN];
+  auto gload = [&](int q, int tile) {
+    const bool isA = q < FM;
+    const int qq = isA ? q : q - FM;
+    // the whole offset in the VGPR: the buffer range check does not include soffset
+    stg[q] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rsrc(isA, tile), (isA ? voffA : voffB) + qq * (isA ? strA : strB),
+                                             0, 0));
+  };
+  auto gload_all = [&](int tile) {
+#pragma unroll
+    for (int q = 0; q < FM + FN; ++q) gload(q, tile);
+  };
+  // pieces [q0, q1) of tile `tile`: mask in registers, write to LDS buffer buf
+  auto gstore = [&](int q, int tile, int buf) {
+    const bool isA = q < FM;
+    const int qq = isA ? q : q - FM;
+    const bool kc = isA ? A_KC : B_KC;
+    const bool tri = isA ? TRIA : TRIB;
+    const int rows = isA ? BM : BN;
+    const int r0 = isA ? m0 : n0;
+    const int k0 = (int)kbeg + GBK * tile;
+    double2 v = stg[q];
+    if (isA) {  // alpha is folded into A
+      v.x *= p.alpha;
+      v.y *= p.alpha;
+    }
+    if (kc) {  // elements (row, gk), (row, gk + 1); K tail; triangle: zero for k > row
+      const int gk = k0 + 2 * (t & 7);
+      const int row = r0 + (t >> 3) + 32 * qq;
+      const bool ok0 = gk < K && (!tri || gk <= row);
+      const bool ok1 = gk + 1 < K && (!tri || gk + 1 <= row);
+      v.x = ok0 ? v.x : 0.0;
+      v.y = ok1 ? v.y : 0.0;
+    } else if (tri) {  // elements (gk, col), (gk, col + 1); triangle: zero for col > k
+      const int half = rows / 2;
+      const int gk = k0 + t / half + (256 / half) * qq;
+      const int col = r0 + 2 * (t % half);
+      v.x = col <= gk ? v.x : 0.0;
+      v.y = col + 1 <= gk ? v.y : 0.0;
+    }
+    *reinterpret_cast<double2*>(smem + buf * SE + (isA ? lA : lB) + 512 * qq) = v;
+  };
+
+  // ---- fragments ----
+  // KC: fa[h][i] = pair 2 fk + h of row (wave rows + 16 i + fr)  -> substeps 2h (.x), 2h + 1 (.y)
+  // MC: fa[s & 1][g] = rows 32 g + 2 fr (+1) of k-row 4 fk + s  -> fragments 2g (.x), 2g + 1 (.y)
+  constexpr int NA = A_KC ? FM : FM / 2, NB_ = B_KC ? FN : FN / 2;
+  double2 fa[2][NA], fb[2][NB_];
+  auto read_kc = [&](double2* dst, int n, const double* base, int row0, int h) {
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const int row = row0 + 16 * i + fr;
+      const int P = 2 * fk + h;
+      dst[i] = *reinterpret_cast<const double2*>(base + row * 16 + 2 * (P ^ ((row >> 1) & 5)));
+    }
+  };
+  auto read_mc = [&](double2* dst, int n, const double* base, int rows, int row0, int s) {
+#pragma unroll
+    for (int g = 0; g < n; ++g)
+      dst[g] = *reinterpret_cast<const double2*>(base + (4 * fk + s) * rows + row0 + 32 * g + 2 * fr);
+  };
+  // reads for substep s of the tile in buffer buf (KC operands only on even substeps)
+  auto read_frags = [&](int s, int buf) {
+    const double* As = smem + buf * SE;
+    const double* Bs = As + AE;
+    if (A_KC) {
+      if ((s & 1) == 0) read_kc(fa[s >> 1], FM, As, wm * 16 * FM, s >> 1);
+    } else {
+      read_mc(fa[s & 1], FM / 2, As, BM, wm * 16 * FM, s);
+    }
+    if (B_KC) {
+      if ((s & 1) == 0) read_kc(fb[s >> 1], FN, Bs, wn * 16 * FN, s >> 1);
+    } else {
+      read_mc(fb[s & 1], FN / 2, Bs, BN, wn * 16 * FN, s);
+    }
+  };
+  auto aval = [&](int s, int i) -> double {
+    if (A_KC) return (s & 1) ? fa[s >> 1][i].y : fa[s >> 1][i].x;
+    return (i & 1) ? fa[s & 1][i >> 1].y : fa[s & 1][i >> 1].x;
+  };
+  auto bval = [&](int s, int j) -> double {
+    if (B_KC) return (s & 1) ? fb[s >> 1][j].y : fb[s >> 1][j].x;
+    return (j & 1) ? fb[s & 1][j >> 1].y : fb[s & 1][j >> 1].x;
+  };
+
+  // ---- C: beta (0 or 1, the host guarantees it) is applied by starting the accumulators at
+  // beta * C; the epilogue stores them straight from the accumulator registers.  Elements outside
+  // C (or above the diagonal of a lower C) get an out-of-range buffer offset: their loads read 0
+  // and their stores are dropped. ----
+  const bool lower = p.uplo_c == VGPOSP_LOWER;
+  double* dst;
+  int ldd;
+  if (p.nsplit > 1) {
+    dst = p.part + (int64_t)zsplit * p.m * p.n;
+    ldd = (int)p.n;
+  } else {
+    dst = p.C;
+    ldd = (int)p.ldc;
+  }
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(dst + (int64_t)m0 * ldd + n0), (short)0, 0x7ffffff8, 0x00020000);
+  const bool with_beta = p.nsplit == 1 && p.beta != 0.0;
+  auto coff = [&](int i, int j, int r) {
+    const int cl = wn * 16 * FN + rs_row<B_KC>(j, fr);
+    const int rl = wm * 16 * FM + rs_row<A_KC>(i, fk + 4 * r);
+    const bool ok = m0 + rl < p.m && n0 + cl < p.n && (!lower || n0 + cl <= m0 + rl);
+    return ok ? (rl * ldd + cl) * 8 : (int)0x7ffffff8;
+  };
+  dbl4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[i][j][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      rc, with_beta ? coff(i, j, r) : 0x7ffffff8, 0, 0));
+
+  auto mfmas = [&](int s, int j0, int j1) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = j0; j < j1; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(aval(s, i), bval(s, j), acc[i][j], 0, 0, 0);
+  };
+
+  // prologue: tile 0 -> LDS buffer 0, tile 1 in flight, substep-0 fragments of tile 0
+  gload_all(0);
+#pragma unroll
+  for (int q = 0; q < FM + FN; ++q) gstore(q, 0, 0);
+  gload_all(1);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  read_frags(0, 0);
+
+  // Schedule (enforced with sched_group_barrier, fenced per phase with sched_barrier): substeps
+  // 0..2 interleave their 32 MFMAs with the next substep's fragment reads and a third of the
+  // staged pieces (mask, LDS write of tile it+1, buffer load of tile it+2); substep 3 runs 3/4 of
+  // its MFMAs, then the LDS barrier, then the first fragment reads of the next tile under the
+  // last quarter of its MFMAs.
+  constexpr int NQ = FM + FN;  // staged pieces, spread over substeps 0..2
+  constexpr int MF = FM * FN;  // MFMAs per substep
+  // LDS reads issued for substep s (s = 0 is issued at the end of the previous tile)
+  constexpr int RD_KC_A = A_KC ? FM : 0, RD_KC_B = B_KC ? FN : 0;
+  constexpr int RD_MC = (A_KC ? 0 : FM / 2) + (B_KC ? 0 : FN / 2);
+  for (int it = 0; it < T; ++it) {
+    const int buf = it & 1;
+    auto phase = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      read_frags(s + 1, buf);
+      constexpr int q0 = (s * NQ) / 3, q1 = ((s + 1) * NQ) / 3;
+#pragma unroll
+      for (int q = q0; q < q1; ++q) {
+        gstore(q, it + 1, buf ^ 1);
+        gload(q, it + 2);
+      }
+      mfmas(s, 0, FN);
+      // MF MFMAs in np groups; each group carries one piece (VALU, LDS write, VMEM) and a share
+      // of the reads (the remainder goes with the last group)
+      constexpr int nrd = RD_MC + (((s + 1) & 1) == 0 ? RD_KC_A + RD_KC_B : 0);
+      constexpr int np = q1 - q0, mg = MF / np, rg = nrd / np, rlast = nrd - rg * (np - 1);
+      static_assert(mg >= 4 + rlast, "MFMA groups too small for the interleave");
+      sgb_group<mg, rg>();
+      if constexpr (np > 2) sgb_group<mg, rg>();
+      if constexpr (np > 3) sgb_group<mg, rg>();
+      if constexpr (np > 4) sgb_group<mg, rg>();
+      static_assert(np <= 5, "at most 5 pieces per phase");
+      sgb_group<mg, rlast>();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    phase(std::integral_constant<int, 0>{});
+    phase(std::integral_constant<int, 1>{});
+    phase(std::integral_constant<int, 2>{});
+    mfmas(3, 0, FN - FN / 4);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags(0, buf ^ 1);
+    mfmas(3, FN - FN / 4, FN);
+    sgb_tail<RD_MC + RD_KC_A + RD_KC_B, FM * (FN / 4)>();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---- epilogue: plain stores; an element outside C (or above the diagonal of a lower C) is
+  // sent to a per-lane sink slot instead (no branches around the accumulator reads).  (A buffer
+  // store of an accumulator element miscompiles: every element of the dbl4 was stored from its
+  // first register pair.) ----
+  double* const cbase = dst + (int64_t)m0 * ldd + n0;
+  double* const sink = g_rs_sink + lane;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int off = coff(i, j, r);
+        double* const ptr = off != (int)0x7ffffff8 ? cbase + off / 8 : sink;
+        *ptr = acc[i][j][r];
+      }
+}
+
 template <int CFG, bool TA, bool TB, bool TRIA, bool TRIB>
 static void launch_one(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn) {
   hipLaunchKernelGGL((gemm_glds_kernel<TA, TB, TRIA, TRIB, CFG>), g1, dim3(64 * GemmCfg<CFG>::NW),
@@ -494,7 +972,7 @@ static void launch_one(dim3 g1, hipStream_t stream, const GemmParams& p, int tm,
 }
 
 // every (transa, transb, tri_a, tri_b) combination: the kernel's K-range and mask logic is
-// generic in the four flags.
+// generic in the four flags.  The 256x128 configurations are instantiated for plain operands only.
 template <int CFG, bool TA, bool TB>
 static void launch_tri(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn, int tri_a,
                        int tri_b) {
@@ -502,6 +980,28 @@ static void launch_tri(dim3 g1, hipStream_t stream, const GemmParams& p, int tm,
   if (tri_a && tri_b) return launch_one<1, TA, TB, true, true>(g1, stream, p, tm, tn);
   if (tri_a) return launch_one<1, TA, TB, true, false>(g1, stream, p, tm, tn);
   launch_one<1, TA, TB, false, true>(g1, stream, p, tm, tn);
+}
+
+template <int FM, int FN, bool TA, bool TB>
+static void launch_rs_tri(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn, int tri_a,
+                          int tri_b) {
+  if (tri_a && tri_b)
+    hipLaunchKernelGGL((gemm_rs_kernel<FM, FN, TA, TB, true, true>), g1, dim3(256), 0, stream, p, tm, tn);
+  else if (tri_a)
+    hipLaunchKernelGGL((gemm_rs_kernel<FM, FN, TA, TB, true, false>), g1, dim3(256), 0, stream, p, tm, tn);
+  else if (tri_b)
+    hipLaunchKernelGGL((gemm_rs_kernel<FM, FN, TA, TB, false, true>), g1, dim3(256), 0, stream, p, tm, tn);
+  else
+    hipLaunchKernelGGL((gemm_rs_kernel<FM, FN, TA, TB, false, false>), g1, dim3(256), 0, stream, p, tm, tn);
+}
+
+template <int FM, int FN>
+static void launch_rs(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn, int transa,
+                      int transb, int tri_a, int tri_b) {
+  if (!transa && !transb) launch_rs_tri<FM, FN, false, false>(g1, stream, p, tm, tn, tri_a, tri_b);
+  else if (!transa) launch_rs_tri<FM, FN, false, true>(g1, stream, p, tm, tn, tri_a, tri_b);
+  else if (!transb) launch_rs_tri<FM, FN, true, false>(g1, stream, p, tm, tn, tri_a, tri_b);
+  else launch_rs_tri<FM, FN, true, true>(g1, stream, p, tm, tn, tri_a, tri_b);
 }
 
 template <int CFG>
@@ -625,6 +1125,28 @@ static int gemv_splits(int64_t m, int64_t k, int transa) {
   return (int)std::max<int64_t>(std::min<int64_t>(s, 4096), 1);
 }
 
+int g_fast_gemm = [] {  // 0 forces the register-staged reference kernel (VGPOSP_GEMM_REF=1)
+  const char* e = getenv("VGPOSP_GEMM_REF");
+  return e && e[0] == '1' ? 0 : 1;
+}();
+// 256x128 configurations (gemm_glds_kernel CFG 2 / 3) only on request, VGPOSP_GEMM_CFG=2 or 3,
+// for full-C launches with at least two rounds of workgroups (measurements in DESIGN.md §4).
+static const int g_prio = [] {
+  const char* e = getenv("VGPOSP_GEMM_PRIO");
+  return e ? atoi(e) : 0;
+}();
+static const int g_cfg = [] {
+  const char* e = getenv("VGPOSP_GEMM_CFG");
+  return (e && (e[0] == '2' || e[0] == '3')) ? e[0] - '0' : 1;
+}();
+
+// one-wave-per-SIMD register-staged kernel (gemm_rs_kernel): VGPOSP_GEMM_RS=1 -> 128x256 tiles,
+// 2 -> 256x128 tiles, 0 -> off
+static const int g_rs = [] {
+  const char* e = getenv("VGPOSP_GEMM_RS");
+  return e ? atoi(e) : 0;
+}();
+
 static bool aligned16(const void* ptr, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(ptr) % 16 == 0) && (ld % 2 == 0);
 }
@@ -660,11 +1182,71 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     }
     return 0;
   }
-  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr};
+  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr,
+               g_prio};
   const int va = aligned16(A, lda), vb = aligned16(B, ldb);
   const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
-  if (va && vb && even) {
-    const int tm = (int)ceil_div(m, GBM), tn = (int)ceil_div(n, GBN);
+  // rs kernel: 32-bit buffer offsets (256 rows x ld x 8 bytes < 2^31), beta folded into the
+  // accumulator start (0 or 1 only)
+  const int64_t ldmax = (nsplit > 1 && part != nullptr) ? std::max(std::max(lda, ldb), n) : std::max(std::max(lda, ldb), ldc);
+  const bool rs_ok = m < (1 << 30) && n < (1 << 30) && k < (1 << 30) && ldmax < (1 << 20) &&
+                     (beta == 0.0 || beta == 1.0);
+  if (va && vb && even && g_fast_gemm && g_rs && rs_ok) {
+    const int FM = g_rs == 2 ? 8 : 4, FN = 12 - FM, BM = 32 * FM, BN = 32 * FN;
+    const int tm = (int)ceil_div(m, BM), tn = (int)ceil_div(n, BN);
+    int64_t nblk = (int64_t)tm * tn;
+    if (uplo_c == VGPOSP_LOWER) {
+      if (BM >= BN) nblk = (int64_t)tm * (tm + 1);
+      else {
+        nblk = 0;
+        for (int i = 0; i < tm; ++i) nblk += i / 2 + 1;
+      }
+    }
+    const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
+    const double fl = 2.0 * (double)k * outs * ((tri_a && tri_b) ? (1.0 / 3.0) : (tri_a || tri_b) ? 0.5 : 1.0);
+    if (nsplit > 1 && part != nullptr) {
+      p.nblk = (int)nblk;
+      p.kchunk = ceil_div(ceil_div(k, nsplit), GBK) * GBK;
+      p.nsplit = (int)ceil_div(k, p.kchunk);
+      p.part = part;
+    }
+    ProfScope ps("gemm_f64", stream, fl,
+                 8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    static const bool shapes = getenv("VGPOSP_PROF_SHAPES") != nullptr;
+    char shape_name[96];
+    if (shapes && prof_on())
+      snprintf(shape_name, sizeof(shape_name), "gemm:%lldx%lldx%lld:%c%c%c%c%c:s%d", (long long)m,
+               (long long)n, (long long)k, transa ? 'T' : 'N', transb ? 'T' : 'N',
+               uplo_c == VGPOSP_LOWER ? 'L' : 'F', tri_a ? 'a' : '-', tri_b ? 'b' : '-', p.nsplit);
+    ProfScope pshape(shape_name, stream, fl, 0.0, shapes && prof_on());
+    dim3 g1((unsigned)(nblk * p.nsplit));
+    if (FM == 4) launch_rs<4, 8>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    else launch_rs<8, 4>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    VG_LAUNCH_CHECK();
+    static const bool dbg_sync = getenv("VGPOSP_GEMM_SYNC") != nullptr;  // debugging aid
+    if (dbg_sync) {
+      const hipError_t e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) {
+        fprintf(stderr, "gemm_rs fault: m=%lld n=%lld k=%lld ta=%d tb=%d uplo=%d tri=%d%d lda=%lld ldb=%lld ldc=%lld "
+                "beta=%g splits=%d A=%p B=%p C=%p\n", (long long)m, (long long)n, (long long)k, transa, transb,
+                uplo_c, tri_a, tri_b, (long long)lda, (long long)ldb, (long long)ldc, beta, p.nsplit, (const void*)A,
+                (const void*)B, (void*)C);
+        set_error("gemm_rs fault: %s", hipGetErrorString(e));
+        return VGPOSP_E_HIP;
+      }
+    }
+    if (p.nsplit > 1) {
+      hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(m * n, 256)), dim3(256),
+                         0, stream, m, n, p.nsplit, part, beta, C, ldc, uplo_c == VGPOSP_LOWER);
+      VG_LAUNCH_CHECK();
+    }
+    return 0;
+  }
+  if (va && vb && even && g_fast_gemm) {
+    // 256x128 tiles for full-C launches with at least two rounds of workgroups, on request
+    const int cfg = (uplo_c == VGPOSP_FULL && g_cfg > 1 && !tri_a && !tri_b &&
+                     ceil_div(m, 2 * GBM) * ceil_div(n, GBN) >= 512) ? g_cfg : 1;
+    const int tm = (int)ceil_div(m, GBM * (cfg == 1 ? 1 : 2)), tn = (int)ceil_div(n, GBN);
     const int64_t nblk = (uplo_c == VGPOSP_LOWER) ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
     const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
     // algorithmic flops: a triangular operand halves the useful products
@@ -677,8 +1259,18 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     }
     ProfScope ps("gemm_f64", stream, fl,
                  8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    // optional per-shape breakdown (VGPOSP_PROF_SHAPES=1): "gemm:MxNxK:flags:splits"
+    static const bool shapes = getenv("VGPOSP_PROF_SHAPES") != nullptr;
+    char shape_name[96];
+    if (shapes && prof_on())
+      snprintf(shape_name, sizeof(shape_name), "gemm:%lldx%lldx%lld:%c%c%c%c%c:s%d", (long long)m,
+               (long long)n, (long long)k, transa ? 'T' : 'N', transb ? 'T' : 'N',
+               uplo_c == VGPOSP_LOWER ? 'L' : 'F', tri_a ? 'a' : '-', tri_b ? 'b' : '-', p.nsplit);
+    ProfScope pshape(shape_name, stream, fl, 0.0, shapes && prof_on());
     dim3 g1((unsigned)(nblk * p.nsplit));
-    launch_glds<1>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    if (cfg == 2) launch_glds<2>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    else if (cfg == 3) launch_glds<3>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
+    else launch_glds<1>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     VG_LAUNCH_CHECK();
     if (p.nsplit > 1) {
       hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(m * n, 256)), dim3(256),
