@@ -7,10 +7,11 @@ One step = the whole job for ONE placement problem, with the grid points already
   -> fused Cholesky + inverse of Sigma             (potrf sweep, fp64 MFMA-bound, 2N^3/3 flops)
   -> k = 50 lazy-greedy selections                 (per round one HBM-bound triangular mat-vec)
 value = placements per second of that job.  With --gpus N the SAME problem is candidate-sharded
-over the N ranks (vgposp_amd.sharded_placement over RCCL: per round one all-gather of the delta
-slabs and one pivot all-reduce); the O(N^3) factorization is replicated on every rank (SURVEY
-§8(e): "Cholesky at N <= 65k: replicas only"), so this is strong scaling whose speed-up that
-replicated init bounds (DESIGN.md §6).  The timed loop runs with the library's event timing OFF;
+over the N ranks (vgposp_amd.sharded_placement over RCCL): every rank factors Sigma (the O(N^3)
+Cholesky is replicated, SURVEY §8(e) "replicas only"), forms L^-1 only in its own candidate
+columns (1/N of the inverse), and per round all-reduces the pick's column of L^-1, all-gathers the
+delta slabs and all-reduces the pivot row.  Strong scaling whose speed-up the replicated Cholesky
+bounds (DESIGN.md §6).  The timed loop runs with the library's event timing OFF;
 the roofline numbers come from one more, profiled, step.
 
 Also reported: fp64 Cholesky GF/s (plain potrf of the same Sigma, N^3/3 flops); config C4 (the
@@ -372,7 +373,7 @@ def main():
                 g.step(lazy=True)
         selected = g.selected
     else:
-        sh = ShardedGreedyPlacement(HipGreedyBackend(Sigma, k))
+        sh = ShardedGreedyPlacement(HipGreedyBackend(Sigma, k), partition_inverse=True)
         g = sh.b.g
 
         def run_rounds():
@@ -497,8 +498,8 @@ def main():
         "config": {"workload": f"{shape[0]}x{shape[1]}x{shape[2]} jittered grid (N={N}), "
                                f"{args.kernel.upper()} kernel amp=1 ls=2h noise={args.noise}+1e-6, "
                                f"k={k} lazy-greedy MI placements, dense-exact, one problem"
-                               + (f" candidate-sharded over {world} ranks (RCCL), factorization "
-                                  "replicated" if world > 1 else ""),
+                               + (f" candidate-sharded over {world} ranks (RCCL), Cholesky "
+                                  "replicated, inverse partitioned" if world > 1 else ""),
                    "N": N, "k": k, "parallelism": f"candidates{world}" if world > 1 else "single",
                    "rccl_world_size": world if world > 1 else None},
         "cholesky_gflops": chol_gflops,

@@ -249,6 +249,26 @@ int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda, int kmax, 
 int vgposp_greedy_select(int64_t n, int kmax, int round, int lazy, int64_t c0, int64_t c1,
                          int64_t* selected, double* sel_delta, int64_t* evals, void* ws,
                          size_t ws_bytes, void* stream);
+/* Partitioned inverse for one problem sharded over R ranks (the O(N^3) factorization is replicated,
+ * the inverse is not): vgposp_greedy_init_slab factors Sigma like vgposp_greedy_init_ex but forms
+ * L^-1 only in columns [c0, c1) (the rank's candidate slab; c0 and c1 multiples of 128 or c1 = n),
+ * about 1/R of the inverse's flops; tmp: vgposp_greedy_slab_tmp_bytes(n, c0, c1) bytes.  Per round
+ * the owner of the last pick's column then provides it: vgposp_greedy_extract writes xcol = that
+ * column of L^-1 if the pick is in [own0, own1) and zeros otherwise, the caller sum-all-reduces
+ * xcol (vgposp_greedy_xcol gives its device address) and runs vgposp_greedy_update_ex with
+ * extract = 0.  vgposp_greedy_update(...) == vgposp_greedy_update_ex(..., extract = 1, ...). */
+size_t vgposp_greedy_slab_tmp_bytes(int64_t n, int64_t c0, int64_t c1);
+int vgposp_greedy_init_slab(double* Sigma, int64_t n, int64_t lda, int kmax, double jitter,
+                            double threshold, double cache_init, int64_t c0, int64_t c1,
+                            double* tmp, size_t tmp_bytes, int* info, void* ws, size_t ws_bytes,
+                            void* stream);
+int vgposp_greedy_extract(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
+                          int64_t own0, int64_t own1, const int64_t* selected, void* ws,
+                          size_t ws_bytes, void* stream);
+int vgposp_greedy_update_ex(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
+                            int64_t c0, int64_t c1, const int64_t* selected, int extract, void* ws,
+                            size_t ws_bytes, void* stream);
+int vgposp_greedy_xcol(void* ws, int64_t n, int kmax, double** xcol);
 /* Device pointers into the workspace: the full delta vector [n] and the pivot buffer. */
 int vgposp_greedy_buffers(void* ws, int64_t n, int kmax, double** delta, double** piv,
                           int64_t* piv_len);

@@ -41,7 +41,25 @@ class NumpyGreedyBackend:
         self.selected = []
         self.sel_delta = []
 
-    def update(self, rnd, c0, c1):
+    def init_slab(self, c0, c1):
+        """Partitioned inverse: only columns [c0, c1) of L^-1 exist on this rank (NaN elsewhere, so
+        any use of another rank's column shows up)."""
+        self.init()
+        own = np.zeros(self.n, dtype=bool)
+        own[c0:c1] = True
+        self.M[:, ~own] = np.nan
+        self.colsq = np.where(own, self.colsq, np.nan)
+        self._xcol = torch.zeros(self.n, dtype=torch.float64)
+
+    def extract(self, rnd, own0, own1):
+        a = self.selected[rnd - 1]
+        x = self._xcol.numpy()
+        x[:] = self.M[:, a] if own0 <= a < own1 else 0.0
+
+    def xcol(self):
+        return self._xcol
+
+    def update(self, rnd, c0, c1, extract=True):
         idx = np.arange(c0, c1)
         if rnd == 0:
             self.prec[idx] = self.colsq[idx]
@@ -49,7 +67,8 @@ class NumpyGreedyBackend:
         else:
             a, t1 = self.selected[rnd - 1], rnd - 1
             piv = self._piv.numpy()
-            q = self.M[:, idx].T @ self.M[:, a]
+            xa = self.M[:, a] if extract else self._xcol.numpy()
+            q = self.M[:, idx].T @ xa
             s = self.S[idx, a].copy()
             s -= piv[2:2 + t1] @ self.W[:t1][:, idx]
             q -= piv[2 + t1:2 + 2 * t1] @ self.V[:t1][:, idx]

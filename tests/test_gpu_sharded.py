@@ -30,7 +30,7 @@ def _grid_cov():
     return ogp.kernel_matrix("eq", X, X, 1.0, 2 * grid_spacing((12, 10, 9)))[0] + 0.010001 * np.eye(len(X))
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, partition):
     import torch
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -41,19 +41,51 @@ def _worker(rank, world, port, out):
         res = {}
         for name in ["spd40", "grid654", "grid8"]:
             e = CASES[name]
-            res[name] = [int(a) for a in placement_algorithm_2_sharded(placement_cov(name, e), e["k"])]
-        res["grid1080"] = [int(a) for a in placement_algorithm_2_sharded(_grid_cov(), 12)]
+            res[name] = [int(a) for a in placement_algorithm_2_sharded(
+                placement_cov(name, e), e["k"], partition_inverse=partition)]
+        res["grid1080"] = [int(a) for a in placement_algorithm_2_sharded(
+            _grid_cov(), 12, partition_inverse=partition)]
         out[rank] = res
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_two_ranks_on_gpu():
+@pytest.mark.parametrize("partition", [True, False])
+def test_sharded_two_ranks_on_gpu(partition):
+    """partition=True: each rank forms only its slab's columns of L^-1 (vgposp_greedy_init_slab;
+    grid1080 splits at column 256) and gets the pick's column by the xcol all-reduce."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, partition), nprocs=2, join=True)
     exp_grid = op.placement_lazy_precision(_grid_cov(), 12)
     for r in range(2):
         for name in ["spd40", "grid654", "grid8"]:
             assert out[r][name] == CASES[name]["alg2"], (r, name)
         assert out[r]["grid1080"] == exp_grid
+
+
+@pytest.mark.parametrize("n,c0,c1", [(3000, 0, 1024), (3000, 1024, 2048), (3000, 2048, 3000),
+                                     (3000, 0, 3000), (700, 128, 256)])
+def test_partial_inverse_columns(n, c0, c1):
+    """vgposp_greedy_init_slab: columns [c0, c1) of L^-1 (rows >= c0) equal the fused full
+    inverse's; every other entry of the buffer keeps the factor L or Sigma."""
+    import torch
+    from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    from vgposp_amd.sharded_placement import HipGreedyBackend
+    X = np.random.default_rng(3).uniform(-2, 2, (n, 3))
+    S = ogp.kernel_matrix("eq", X, X, 1.0, 0.7)[0] + 0.02 * np.eye(n)
+    full = GreedyPlacement(S, 4, copy=True).init()
+    b = HipGreedyBackend(S, 4, copy=True)
+    b.init_slab(c0, c1)
+    torch.cuda.synchronize()
+    full.check()
+    b.g.check()
+    Mf = full.S.cpu().numpy()
+    Mp = b.g.S.cpu().numpy()
+    lo = np.tril(np.ones((n, n), dtype=bool))
+    cols = np.zeros((n, n), dtype=bool)
+    cols[:, c0:c1] = True
+    sel = lo & cols
+    np.testing.assert_allclose(Mp[sel], Mf[sel], rtol=1e-10, atol=1e-12 * np.abs(Mf[sel]).max())
+    up = ~lo
+    np.testing.assert_array_equal(Mp[up], S[up])

@@ -24,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, names, lazy, out):
+def _worker(rank, world, port, names, lazy, out, partition=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -35,7 +35,8 @@ def _worker(rank, world, port, names, lazy, out):
         for name in names:
             e = CASES[name]
             cov = placement_cov(name, e)
-            sh = ShardedGreedyPlacement(NumpyGreedyBackend(cov, e["k"]))
+            sh = ShardedGreedyPlacement(NumpyGreedyBackend(cov, e["k"]), partition_inverse=partition,
+                                        align=4)
             A, _, _ = sh.run(e["k"], lazy=lazy)
             res[name] = [int(a) for a in A]
         out[rank] = res
@@ -54,6 +55,31 @@ def test_sharded_matches_reference(world, lazy):
         for name in names:
             exp = CASES[name]["alg2" if lazy else "alg1"]
             assert out[r][name] == exp, (r, name)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_partitioned_inverse_matches_reference(world):
+    """Each rank forms only its slab's columns of L^-1 (the others are NaN in the numpy backend);
+    the pick's column reaches every rank through the xcol sum-all-reduce."""
+    names = ["cov4x4", "spd40", "grid4", "grid654"]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), names, True, out, True), nprocs=world, join=True)
+    for r in range(world):
+        for name in names:
+            assert out[r][name] == CASES[name]["alg2"], (r, name)
+
+
+def test_inverse_slabs():
+    from vgposp_amd.sharded_placement import inverse_slabs
+    n = 65536
+    for world in (1, 2, 4, 8):
+        sl = inverse_slabs(n, world)
+        assert sl[0][0] == 0 and sl[-1][1] == n
+        assert all(a % 128 == 0 and a <= b for a, b in sl)
+        work = [(n - a) ** 3 - (n - b) ** 3 for a, b in sl]
+        assert max(work) / min(work) < 1.05
+    assert inverse_slabs(100, 2) == [(0, 0), (0, 100)]
 
 
 def test_slab_bounds_balanced():

@@ -111,6 +111,14 @@ SIGNATURES = {
                                     _c_void_p, _size, _c_void_p]),
     "vgposp_greedy_select": (_i32, [_i64, _i32, _i32, _i32, _i64, _i64, _c_void_p, _c_void_p,
                                     _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_slab_tmp_bytes": (_size, [_i64, _i64, _i64]),
+    "vgposp_greedy_init_slab": (_i32, [_c_void_p, _i64, _i64, _i32, _f64, _f64, _f64, _i64, _i64,
+                                       _c_void_p, _size, _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_extract": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i64, _i64, _c_void_p,
+                                     _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_update_ex": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i64, _i64, _c_void_p,
+                                       _i32, _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_xcol": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p)]),
     "vgposp_greedy_buffers": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p),
                                      ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),
     "vgposp_greedy_step": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,

@@ -25,6 +25,9 @@ namespace vgposp {
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
               void* ws, hipStream_t stream);
 size_t potrf_ws_bytes(int64_t n);
+int partial_inverse(double* A, int64_t n, int64_t lda, int64_t c0, int64_t c1, double* tmp,
+                    void* ws, hipStream_t s);
+size_t partial_inverse_tmp_bytes(int64_t n, int64_t c0, int64_t c1);
 
 constexpr int RC = 512;     // rows per chunk of the transposed mat-vec
 constexpr int CT = 256;     // columns per mat-vec workgroup
@@ -123,12 +126,16 @@ __global__ void greedy_init_kernel(double* S, int64_t n, int64_t lda, double jit
   }
 }
 
-// x = M e_a restricted to rows >= a (the selected column of L^-1), a = selected[round-1].
+// x = M e_a restricted to rows >= a (the selected column of L^-1), a = selected[round-1].  With a
+// partitioned inverse only the owner of column a holds it: the others write zeros (the caller
+// sum-all-reduces xcol), i.e. the column is taken only when a is in [own0, own1).
 __global__ void greedy_extract_kernel(const double* M, int64_t n, int64_t lda,
-                                      const int64_t* selected, int round, double* xcol) {
+                                      const int64_t* selected, int round, double* xcol,
+                                      int64_t own0, int64_t own1) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t a = selected[round - 1];
-  if (r < n) xcol[r] = (r >= a) ? M[r * lda + a] : 0.0;
+  const bool own = a >= own0 && a < own1;
+  if (r < n) xcol[r] = (own && r >= a) ? M[r * lda + a] : 0.0;
 }
 
 // part[rc][c] = sum_{r in chunk rc, r >= max(c, a)} M[r][c] * f(r, c)
@@ -501,9 +508,9 @@ static int greedy_check(const char* fn, const double* Sigma, int64_t n, int64_t 
   return 0;
 }
 
-extern "C" int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda, int kmax,
-                                    int round, int64_t c0, int64_t c1, const int64_t* selected,
-                                    void* ws, size_t ws_bytes, void* stream) {
+extern "C" int vgposp_greedy_update_ex(const double* Sigma, int64_t n, int64_t lda, int kmax,
+                                       int round, int64_t c0, int64_t c1, const int64_t* selected,
+                                       int extract, void* ws, size_t ws_bytes, void* stream) {
   clear_error();
   GreedyWS w;
   int rc = greedy_check(__func__, Sigma, n, lda, kmax, round, ws, ws_bytes, &w);
@@ -513,9 +520,11 @@ extern "C" int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda,
   hipStream_t s = as_stream(stream);
   if (c1 == c0) return 0;
   if (round > 0) {
-    hipLaunchKernelGGL(greedy_extract_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
-                       Sigma, n, lda, selected, round, w.xcol);
-    VG_LAUNCH_CHECK();
+    if (extract) {
+      hipLaunchKernelGGL(greedy_extract_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                         Sigma, n, lda, selected, round, w.xcol, (int64_t)0, n);
+      VG_LAUNCH_CHECK();
+    }
     dim3 g((unsigned)ceil_div(c1 - (c0 & ~(int64_t)1), TRMV_COLS), (unsigned)ceil_div(n, RC));
     const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);
     // algorithmic: the lower triangle of L^-1 in rows >= a, columns [c0, c1) (a is device-side;
@@ -533,6 +542,89 @@ extern "C" int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda,
                        lda, selected, round, w, c0, c1);
     VG_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+extern "C" int vgposp_greedy_update(const double* Sigma, int64_t n, int64_t lda, int kmax,
+                                    int round, int64_t c0, int64_t c1, const int64_t* selected,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  return vgposp_greedy_update_ex(Sigma, n, lda, kmax, round, c0, c1, selected, 1, ws, ws_bytes,
+                                 stream);
+}
+
+extern "C" int vgposp_greedy_extract(const double* Sigma, int64_t n, int64_t lda, int kmax,
+                                     int round, int64_t own0, int64_t own1,
+                                     const int64_t* selected, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  clear_error();
+  GreedyWS w;
+  int rc = greedy_check(__func__, Sigma, n, lda, kmax, round, ws, ws_bytes, &w);
+  if (rc) return rc;
+  VG_CHECK_ARG(round >= 1, 5);
+  VG_CHECK_ARG(own0 >= 0 && own0 <= own1 && own1 <= n, 6);
+  VG_CHECK_ARG(selected != nullptr, 8);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(greedy_extract_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                     Sigma, n, lda, selected, round, w.xcol, own0, own1);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t vgposp_greedy_slab_tmp_bytes(int64_t n, int64_t c0, int64_t c1) {
+  if (n <= 0 || c0 < 0 || c1 <= c0 || c1 > n) return 0;
+  return partial_inverse_tmp_bytes(n, c0, c1);
+}
+
+extern "C" int vgposp_greedy_init_slab(double* Sigma, int64_t n, int64_t lda, int kmax,
+                                       double jitter, double threshold, double cache_init,
+                                       int64_t c0, int64_t c1, double* tmp, size_t tmp_bytes,
+                                       int* info, void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(Sigma != nullptr, 1);
+  VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
+  VG_CHECK_ARG(jitter >= 0.0 && jitter < 1e300, 5);
+  VG_CHECK_ARG(threshold >= 0.0, 6);
+  VG_CHECK_ARG(cache_init == cache_init, 7);
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c0 % 128 == 0, 8);
+  VG_CHECK_ARG(c1 <= n && (c1 % 128 == 0 || c1 == n), 9);
+  VG_CHECK_ARG(c1 == c0 || (tmp != nullptr && tmp_bytes >= partial_inverse_tmp_bytes(n, c0, c1)),
+               10);
+  VG_CHECK_ARG(info != nullptr, 12);
+  VG_CHECK_ARG(ws != nullptr, 13);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  if (ws_bytes < w.bytes) {
+    set_error("vgposp_greedy_init_slab: workspace %zu < %zu bytes", ws_bytes, w.bytes);
+    return VGPOSP_E_WS;
+  }
+  hipStream_t s = as_stream(stream);
+  VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
+  hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
+                     n, lda, jitter, threshold, cache_init, w);
+  VG_LAUNCH_CHECK();
+  void* fws = greedy_fact_ws(ws, w, n);
+  int rc = potrf_one(Sigma, n, lda, /*invert=*/0, nullptr, info, fws, s);
+  if (rc) return rc;
+  if (c1 == c0) return 0;
+  if ((rc = partial_inverse(Sigma, n, lda, c0, c1, tmp, fws, s))) return rc;
+  // Q_ii = |M e_i|^2 for the slab's columns -> part (reduced in the round-0 update)
+  dim3 g((unsigned)ceil_div(c1 - (c0 & ~(int64_t)1), TRMV_COLS), (unsigned)ceil_div(n, RC));
+  const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);
+  ProfScope ps("greedy_colsq", s, 0.0, 0.0);
+  hipLaunchKernelGGL(greedy_trmv_kernel<true>, g, dim3(CT), 0, s, Sigma, n, lda, nullptr, 0,
+                     nullptr, w.part, c0, c1, vec);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_greedy_xcol(void* ws, int64_t n, int kmax, double** xcol) {
+  clear_error();
+  VG_CHECK_ARG(ws != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(kmax >= 1, 3);
+  VG_CHECK_ARG(xcol != nullptr, 4);
+  *xcol = greedy_layout(ws, n, kmax).xcol;
   return 0;
 }
 

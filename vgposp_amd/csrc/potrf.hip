@@ -459,9 +459,11 @@ static int ensure_leaf_attr() {
   return 0;
 }
 
-int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
-              void* ws, hipStream_t stream) {
-  if (int rc = ensure_leaf_attr()) return rc;
+static int trsm_left_rec(const Fact& f, const double* Lp, int64_t ldl, int64_t n, int64_t col0,
+                         int trans, double* B, int64_t m, int64_t ldb);
+
+static Fact make_fact(int64_t n, int64_t lda, void* ws, double* diag_out, int* info,
+                      hipStream_t stream) {
   const int64_t leaves = (n + NB - 1) / NB;
   const int64_t n1 = n > NB ? split_point(n) : 0;
   double* base = static_cast<double*>(ws);
@@ -470,10 +472,48 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
   double* xinv = blocks ? work + n1 * (n - n1) : nullptr;
   double* tmp = blocks ? xinv + n * NBI : nullptr;
   double* part = n > NB ? work + n1 * (n - n1) + (blocks ? 2 * n * NBI : 0) : nullptr;
-  Fact f{lda, base, work, xinv, tmp, diag_out, info, part, stream};
+  return Fact{lda, base, work, xinv, tmp, diag_out, info, part, stream};
+}
+
+int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
+              void* ws, hipStream_t stream) {
+  if (int rc = ensure_leaf_attr()) return rc;
+  const bool blocks = n > NBI;
+  Fact f = make_fact(n, lda, ws, diag_out, info, stream);
   int rc = potrf_rec(f, A, n, 0, blocks);
   if (rc || !invert) return rc;
   return trtri_rec(f, A, lda, n, 0, blocks);
+}
+
+size_t partial_inverse_tmp_bytes(int64_t n, int64_t c0, int64_t c1) {
+  return (size_t)((n - c1) * (c1 - c0) + NB * (c1 - c0)) * sizeof(double);
+}
+
+// After potrf_one(A, invert = 0) with the same ws (its leaf inverses): the lower part of columns
+// [c0, c1) of A (rows >= c0) <- the same columns of L^-1, the rest of L untouched.  With
+//   L = [L11 0; L21 L22] split at c1 (L11 = L[c0:c1, c0:c1], L21 = L[c1:, c0:c1]):
+//   X11 = L11^-1 (in place, leaf-level trtri), X21 = -L22^-1 (L21 X11) (a GEMM and a TRSM through
+//   tmp).  About the flops of this slab's share of a full trtri (a candidate-sharded rank forms
+//   only the columns of L^-1 its candidates need).  c0 and c1 are multiples of 128, or c1 = n.
+int partial_inverse(double* A, int64_t n, int64_t lda, int64_t c0, int64_t c1, double* tmp,
+                    void* ws, hipStream_t s) {
+  const int64_t w = c1 - c0, m2 = n - c1;
+  if (w <= 0) return 0;
+  Fact f = make_fact(n, lda, ws, nullptr, nullptr, s);
+  f.tmp = tmp + m2 * w;  // the TRSM leaves' out-of-place scratch: NB x w
+  int rc;
+  double* A11 = A + c0 * lda + c0;
+  if ((rc = trtri_rec(f, A11, lda, w, c0, false))) return rc;
+  if (m2 == 0) return 0;
+  double* L21 = A + c1 * lda + c0;
+  // tmp = -L21 X11  (X11 lower, stored [k][j])
+  if ((rc = pgemm(f, 0, 0, m2, w, w, -1.0, L21, lda, A11, lda, 0.0, tmp, w, VGPOSP_FULL, 0, 1)))
+    return rc;
+  // tmp <- L22^-1 tmp
+  if ((rc = trsm_left_rec(f, A + c1 * lda + c1, lda, m2, c1, 0, tmp, w, w))) return rc;
+  VG_HIP(hipMemcpy2DAsync(L21, lda * sizeof(double), tmp, w * sizeof(double), w * sizeof(double),
+                          m2, hipMemcpyDeviceToDevice, s));
+  return 0;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,9 +1,14 @@
 """Candidate-sharded greedy MI placement across GPUs, one process per GPU.
 
-The candidate set V is cut into R contiguous slabs (balanced by the work of the triangular
-mat-vec: column c of L^-1 has n - c stored rows).  Every rank holds the factored covariance
-(the O(N^3) init is replicated — "replicas only" for the factorization at N <= 65k) and, per round:
+The candidate set V is cut into R contiguous slabs.  Every rank factors the covariance (the
+O(N^3) Cholesky is replicated — "replicas only" for the factorization at N <= 65k).
+With ``partition_inverse=True`` (what bench.py runs) a rank then forms L^-1 only in its own slab's
+columns (vgposp_greedy_init_slab: about 1/R of the inverse's flops, slabs balanced by that work,
+128-aligned); otherwise the fused Cholesky + full inverse is replicated and the slabs balance the
+triangular mat-vec (column c of L^-1 has n - c stored rows).  Per round:
 
+  0. (partitioned inverse) the owner of the last pick's column of L^-1 writes it, the others zeros,
+     and ONE sum-all-reduce of that column (N x 8 bytes) gives every rank the mat-vec's vector;
   1. ``vgposp_greedy_update`` on its slab: W / V rank-1 rows, nom, P_yy and fresh deltas for the
      slab's candidates only (the HBM-bound mat-vec reads only the slab's columns of L^-1);
   2. ONE all-gather of the delta slabs (N x 8 bytes) so every rank holds all fresh deltas;
@@ -45,6 +50,19 @@ def slab_bounds(n, world, balance=True):
     return [(edges[r], edges[r + 1]) for r in range(world)]
 
 
+def inverse_slabs(n, world, align=128):
+    """Contiguous slabs whose columns of L^-1 cost the same to form: the work of columns [0, c) is
+    about n^3 - (n - c)^3, so rank r's boundary is n (1 - (1 - r / world)^(1/3)), rounded to a
+    multiple of ``align`` (vgposp_greedy_init_slab's block boundary)."""
+    edges = [0]
+    for r in range(1, world):
+        c = n * (1.0 - (1.0 - r / world) ** (1.0 / 3.0))
+        c = int(round(c / align)) * align
+        edges.append(int(min(max(c, edges[-1]), n)))
+    edges.append(n)
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
 class HipGreedyBackend:
     """The per-rank device state: a GreedyPlacement plus tensor views of its delta / pivot."""
 
@@ -60,13 +78,37 @@ class HipGreedyBackend:
         self._delta = self.g.ws[d.value - base:d.value - base + 8 * self.n].view(torch.float64)
         self._piv = self.g.ws[p.value - base:p.value - base + 8 * plen.value].view(torch.float64)
 
+        x = ctypes.c_void_p()
+        call("vgposp_greedy_xcol", _p(self.g.ws), self.n, self.kmax, ctypes.byref(x))
+        self._xcol = self.g.ws[x.value - base:x.value - base + 8 * self.n].view(torch.float64)
+        self._tmp = None
+
     def init(self):
         self.g.init()
 
-    def update(self, rnd, c0, c1):
+    def init_slab(self, c0, c1):
+        """Factor Sigma, form L^-1 only in columns [c0, c1) (vgposp_greedy_init_slab)."""
+        from ._lib import query
         g = self.g
-        call("vgposp_greedy_update", _p(g.S), g.n, g.S.stride(0), g.kmax, rnd, c0, c1,
+        need = query("vgposp_greedy_slab_tmp_bytes", g.n, c0, c1)
+        if self._tmp is None or self._tmp.numel() < need:
+            self._tmp = torch.empty(max(need, 8), dtype=torch.uint8, device=g.S.device)
+        call("vgposp_greedy_init_slab", _p(g.S), g.n, g.S.stride(0), g.kmax, *g.params, c0, c1,
+             _p(self._tmp), self._tmp.numel(), _p(g.info), _p(g.ws), g.ws.numel(), _stream())
+        g.rounds = 0
+
+    def extract(self, rnd, own0, own1):
+        g = self.g
+        call("vgposp_greedy_extract", _p(g.S), g.n, g.S.stride(0), g.kmax, rnd, own0, own1,
              _p(g.selected), _p(g.ws), g.ws.numel(), _stream())
+
+    def xcol(self):
+        return self._xcol
+
+    def update(self, rnd, c0, c1, extract=True):
+        g = self.g
+        call("vgposp_greedy_update_ex", _p(g.S), g.n, g.S.stride(0), g.kmax, rnd, c0, c1,
+             _p(g.selected), int(extract), _p(g.ws), g.ws.numel(), _stream())
 
     def select(self, rnd, lazy, c0, c1):
         g = self.g
@@ -85,12 +127,14 @@ class HipGreedyBackend:
 
 
 class ShardedGreedyPlacement:
-    def __init__(self, backend, group=None, balance=True):
+    def __init__(self, backend, group=None, balance=True, partition_inverse=False, align=128):
         self.b = backend
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.slabs = slab_bounds(backend.n, self.world, balance)
+        self.partition = bool(partition_inverse)
+        self.slabs = (inverse_slabs(backend.n, self.world, align) if self.partition else
+                      slab_bounds(backend.n, self.world, balance))
         self.c0, self.c1 = self.slabs[self.rank]
         self.S = max(c1 - c0 for c0, c1 in self.slabs)
         dev = backend.delta().device
@@ -125,18 +169,39 @@ class ShardedGreedyPlacement:
         else:
             dist.all_reduce(p, op=dist.ReduceOp.SUM, group=self.group)
 
+    def _allreduce_xcol(self):
+        """The last pick's column of L^-1: only its owner wrote non-zeros."""
+        if self.world == 1:
+            return
+        x = self.b.xcol()
+        if self.staging:
+            h = x.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            x.copy_(h)
+        else:
+            dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group)
+
     def run(self, k, lazy=True):
-        self.b.init()
+        if self.partition:
+            self.b.init_slab(self.c0, self.c1)
+        else:
+            self.b.init()
         for rnd in range(k):
-            self.b.update(rnd, self.c0, self.c1)
+            if self.partition and rnd > 0:
+                self.b.extract(rnd, self.c0, self.c1)
+                self._allreduce_xcol()
+                self.b.update(rnd, self.c0, self.c1, extract=False)
+            else:
+                self.b.update(rnd, self.c0, self.c1)
             self._allgather_delta()
             self.b.select(rnd, lazy, self.c0, self.c1)
             self._allreduce_piv(rnd)
         return self.b.result()
 
 
-def placement_algorithm_2_sharded(cov_vv, k, group=None, lazy=True):
+def placement_algorithm_2_sharded(cov_vv, k, group=None, lazy=True, partition_inverse=True):
     """placement_algorithm_2 with candidates sharded over the ranks of ``group`` (every rank
     passes the same cov_vv and gets the same list)."""
-    sh = ShardedGreedyPlacement(HipGreedyBackend(cov_vv, k, copy=True), group)
+    sh = ShardedGreedyPlacement(HipGreedyBackend(cov_vv, k, copy=True), group,
+                                partition_inverse=partition_inverse)
     return sh.run(k, lazy)[0]
