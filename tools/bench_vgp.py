@@ -21,7 +21,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from vgposp_amd import _lib
-from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
+from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph, vgp_c5_data
 
 
 def main():
@@ -32,9 +32,14 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--shapes", action="store_true", help="per-shape GEMM / per-kernel dump")
+    ap.add_argument("--c5", action="store_true", help="config C5: 65,536 x 5-D, M = 4^5, B = 8192")
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    X, y, Z = vgp_c3_data(args.n, args.m)
+    if args.c5:
+        X, y, Z = vgp_c5_data()
+        args.batch = 8192
+    else:
+        X, y, Z = vgp_c3_data(args.n, args.m)
     N, B = len(X), args.batch
     train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B)
     rng = np.random.default_rng(1)
