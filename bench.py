@@ -7,11 +7,11 @@ One step = the whole job for ONE placement problem, with the grid points already
   -> fused Cholesky + inverse of Sigma             (potrf sweep, fp64 MFMA-bound, 2N^3/3 flops)
   -> k = 50 lazy-greedy selections                 (per round one HBM-bound triangular mat-vec)
 value = placements per second of that job.  With --gpus N the SAME problem is candidate-sharded
-over the N ranks (vgposp_amd.sharded_placement over RCCL): every rank factors Sigma (the O(N^3)
-Cholesky is replicated, SURVEY §8(e) "replicas only"), forms L^-1 only in its own candidate
-columns (1/N of the inverse), and per round all-reduces the pick's column of L^-1, all-gathers the
-delta slabs and all-reduces the pivot row.  Strong scaling whose speed-up the replicated Cholesky
-bounds (DESIGN.md §6).  The timed loop runs with the library's event timing OFF;
+over the N ranks (vgposp_amd.sharded_placement over RCCL): the ranks factor Sigma together
+(vgposp_amd.dist_cholesky: each large node of the recursive Cholesky has its panel TRSM and SYRK
+split over the ranks, shares all-gathered), each rank forms L^-1 only in its own candidate columns
+(1/N of the inverse), and per round all-reduces the pick's column of L^-1, all-gathers the delta
+slabs and all-reduces the pivot row.  Strong scaling (DESIGN.md §6).  The timed loop runs with the library's event timing OFF;
 the roofline numbers come from one more, profiled, step.
 
 Also reported: fp64 Cholesky GF/s (plain potrf of the same Sigma, N^3/3 flops); config C4 (the
@@ -419,15 +419,29 @@ def main():
 
     # separate plain potrf (N^3/3) for the Cholesky GF/s figure
     chol_gflops = None
+    dist_exchanged_gb = None
     if not args.no_potrf:
         linalg.kernel_matrix(args.kernel, Xd, None, amp_d, ls_d, diag_shift=shift_d, lower=True,
                              out=Sigma[None])
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        linalg.cholesky_(Sigma, invert=False, check=False)
-        ev1.record()
-        torch.cuda.synchronize()
-        chol_gflops = N ** 3 / 3 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+        if world == 1:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            linalg.cholesky_(Sigma, invert=False, check=False)
+            ev1.record()
+            torch.cuda.synchronize()
+            chol_gflops = N ** 3 / 3 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+        else:
+            # the distributed factorization the sharded step runs, over all ranks
+            from vgposp_amd.dist_cholesky import DistCholesky, greedy_cholesky_ops
+            dc = DistCholesky(greedy_cholesky_ops(g))
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dc.factor()
+            torch.cuda.synchronize()
+            barrier()
+            chol_gflops = N ** 3 / 3 / maxtime(time.perf_counter() - t0) / 1e9
+            dist_exchanged_gb = 8.0 * dc.exchanged / 1e9
     del Sigma
     torch.cuda.empty_cache()
 
@@ -499,10 +513,14 @@ def main():
                                f"{args.kernel.upper()} kernel amp=1 ls=2h noise={args.noise}+1e-6, "
                                f"k={k} lazy-greedy MI placements, dense-exact, one problem"
                                + (f" candidate-sharded over {world} ranks (RCCL), Cholesky "
-                                  "replicated, inverse partitioned" if world > 1 else ""),
+                                  "distributed (panel / SYRK shares all-gathered), inverse "
+                                  "partitioned" if world > 1 else ""),
                    "N": N, "k": k, "parallelism": f"candidates{world}" if world > 1 else "single",
                    "rccl_world_size": world if world > 1 else None},
         "cholesky_gflops": chol_gflops,
+        "cholesky_note": ("plain single-GPU potrf of the same Sigma" if world == 1 else
+                          f"distributed potrf over {world} ranks (max-over-ranks time), "
+                          f"{dist_exchanged_gb} GB all-gathered"),
         "roofline": roof,
         "roofline_hbm": hbm,
         "breakdown": breakdown,

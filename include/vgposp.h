@@ -145,6 +145,34 @@ int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t stride, int ba
                        double* diag_out, int* info, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * The Cholesky of ONE matrix distributed over R ranks (one process per GPU) that each hold the
+ * whole matrix: the O(N^3) factorization behind placement_algorithm2.py:151-219's pinv calls,
+ * which the candidate-sharded placement would otherwise replicate on every rank.
+ * The host (vgposp_amd/dist_cholesky.py) walks vgposp_potrf_lower's recursion: a node of size nsub
+ * at column col0 splits at n1 = vgposp_potrf_split(nsub); nodes below a size threshold are factored
+ * whole on every rank (vgposp_potrf_block); above it every rank computes a share of the node's
+ * panel TRSM (vgposp_potrf_panel: rows [r0, r1) of L21 = A21 L11^-T, rows counted from col0 + n1)
+ * and of its SYRK (vgposp_potrf_trailing: rows [b0, b1) of the lower triangle of A22 -= L21 L21^T),
+ * and the ranks all-gather the shares (vgposp_pack_rows / unpack into contiguous buffers, RCCL
+ * all-gather).  ws: a vgposp_potrf_workspace_bytes(n) workspace for the whole n (the leaf and
+ * 512-block inverses are kept at their global columns, as vgposp_potrf_lower leaves them, e.g.
+ * vgposp_greedy_fact_ws's).  col0 is a multiple of 128.
+ * vgposp_pack_rows: rows [r0, r1) x columns [c0, c1) of A (lower = 0) or the lower trapezoid
+ * (columns [c0, r] of row r; lower = 1 needs c0 <= r0, c1 >= r1) <-> buf, packed row after row
+ * (unpack = 1 writes A); vgposp_pack_elems gives the element count.
+ * --------------------------------------------------------------------------------------------- */
+int64_t vgposp_potrf_split(int64_t n);
+int vgposp_potrf_block(double* A, int64_t n, int64_t lda, int64_t col0, int64_t nb, int* info,
+                       void* ws, size_t ws_bytes, void* stream);
+int vgposp_potrf_panel(double* A, int64_t n, int64_t lda, int64_t col0, int64_t nsub, int64_t r0,
+                       int64_t r1, void* ws, size_t ws_bytes, void* stream);
+int vgposp_potrf_trailing(double* A, int64_t n, int64_t lda, int64_t col0, int64_t nsub,
+                          int64_t b0, int64_t b1, void* ws, size_t ws_bytes, void* stream);
+int64_t vgposp_pack_elems(int64_t r0, int64_t r1, int64_t c0, int64_t c1, int lower);
+int vgposp_pack_rows(double* A, int64_t lda, int64_t r0, int64_t r1, int64_t c0, int64_t c1,
+                     int lower, double* buf, int unpack, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Left-side triangular solve with a factor from vgposp_potrf_lower(invert = 0), in place on B:
  *   trans = 0:  B (n x nrhs, ldb) <- L^-1 B        trans = 1:  B <- L^-T B
  * Replaces tf.linalg.triangular_solve(L, ...) inside tfd.GaussianProcess.log_prob and the
@@ -262,6 +290,17 @@ int vgposp_greedy_init_slab(double* Sigma, int64_t n, int64_t lda, int kmax, dou
                             double threshold, double cache_init, int64_t c0, int64_t c1,
                             double* tmp, size_t tmp_bytes, int* info, void* ws, size_t ws_bytes,
                             void* stream);
+/* vgposp_greedy_init_slab in phases, for a factorization the caller runs itself (the distributed
+ * Cholesky above): vgposp_greedy_prepare (saves diag(Sigma), jitter, cache init, info = 0), then the
+ * lower factor of Sigma in place with the potrf workspace vgposp_greedy_fact_ws returns, then
+ * vgposp_greedy_finish_slab (L^-1 in columns [c0, c1) and their column norms). */
+int vgposp_greedy_prepare(double* Sigma, int64_t n, int64_t lda, int kmax, double jitter,
+                          double threshold, double cache_init, int* info, void* ws,
+                          size_t ws_bytes, void* stream);
+int vgposp_greedy_fact_ws(void* ws, int64_t n, int kmax, void** fws, size_t* fws_bytes);
+int vgposp_greedy_finish_slab(double* Sigma, int64_t n, int64_t lda, int kmax, int64_t c0,
+                              int64_t c1, double* tmp, size_t tmp_bytes, void* ws,
+                              size_t ws_bytes, void* stream);
 int vgposp_greedy_extract(const double* Sigma, int64_t n, int64_t lda, int kmax, int round,
                           int64_t own0, int64_t own1, const int64_t* selected, void* ws,
                           size_t ws_bytes, void* stream);

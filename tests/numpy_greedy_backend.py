@@ -16,6 +16,66 @@ def _keymax(vals, idx):
     return int(idx[np.flatnonzero(v == best)[0]])
 
 
+def split_point(n, nb=128):
+    """vgposp_potrf_split: the recursion's split (potrf.hip split_point)."""
+    return nb * (((n + nb - 1) // nb) // 2) if n > nb else 0
+
+
+class NumpyCholeskyOps:
+    """vgposp_potrf_block / _panel / _trailing / pack_rows on a numpy matrix (lower triangle
+    factored in place, the strictly upper triangle never written), for DistCholesky on gloo."""
+
+    def __init__(self, A):
+        self.A = A
+        self.n = A.shape[0]
+        self.device = torch.device("cpu")
+
+    def split(self, n):
+        return split_point(n)
+
+    def block(self, col0, nb):
+        s = slice(col0, col0 + nb)
+        B = np.tril(self.A[s, s])
+        L = np.linalg.cholesky(B + np.tril(B, -1).T)
+        low = np.tril(np.ones((nb, nb), dtype=bool))
+        blk = self.A[s, s]
+        blk[low] = L[low]
+
+    def panel(self, col0, nsub, r0, r1):
+        n1 = split_point(nsub)
+        L11 = np.tril(self.A[col0:col0 + n1, col0:col0 + n1])
+        rows = slice(col0 + n1 + r0, col0 + n1 + r1)
+        cols = slice(col0, col0 + n1)
+        self.A[rows, cols] = np.linalg.solve(L11, self.A[rows, cols].T).T
+
+    def trailing(self, col0, nsub, b0, b1):
+        n1 = split_point(nsub)
+        base = col0 + n1
+        L21 = self.A[base:col0 + nsub, col0:base]
+        upd = L21[b0:b1] @ L21[:b1].T
+        for i in range(b1 - b0):
+            r = b0 + i
+            self.A[base + r, base:base + r + 1] -= upd[i, :r + 1]
+
+    def pack_elems(self, r0, r1, c0, c1, lower):
+        m = r1 - r0
+        if m <= 0:
+            return 0
+        return m * (r0 + 1 - c0) + m * (m - 1) // 2 if lower else m * (c1 - c0)
+
+    def pack(self, r0, r1, c0, c1, lower, buf, unpack):
+        b = buf.numpy()
+        off = 0
+        for r in range(r0, r1):
+            e = r + 1 if lower else c1
+            w = e - c0
+            if unpack:
+                self.A[r, c0:e] = b[off:off + w]
+            else:
+                b[off:off + w] = self.A[r, c0:e]
+            off += w
+
+
 class NumpyGreedyBackend:
     def __init__(self, Sigma, kmax):
         self.S = np.array(Sigma, dtype=np.float64)
@@ -41,10 +101,27 @@ class NumpyGreedyBackend:
         self.selected = []
         self.sel_delta = []
 
+    def prepare(self):
+        self.F = self.S.copy()
+
+    def chol_ops(self):
+        return NumpyCholeskyOps(self.F)
+
+    def finish_slab(self, c0, c1):
+        """After DistCholesky on chol_ops(): the partitioned state from the shared factor."""
+        L = np.tril(self.F)
+        self.init()
+        self.M = np.linalg.inv(L)
+        self.colsq = np.sum(self.M ** 2, axis=0)
+        self._mask_slab(c0, c1)
+
     def init_slab(self, c0, c1):
         """Partitioned inverse: only columns [c0, c1) of L^-1 exist on this rank (NaN elsewhere, so
         any use of another rank's column shows up)."""
         self.init()
+        self._mask_slab(c0, c1)
+
+    def _mask_slab(self, c0, c1):
         own = np.zeros(self.n, dtype=bool)
         own[c0:c1] = True
         self.M[:, ~own] = np.nan

@@ -44,7 +44,7 @@ def _worker(rank, world, port, out, partition):
             res[name] = [int(a) for a in placement_algorithm_2_sharded(
                 placement_cov(name, e), e["k"], partition_inverse=partition)]
         res["grid1080"] = [int(a) for a in placement_algorithm_2_sharded(
-            _grid_cov(), 12, partition_inverse=partition)]
+            _grid_cov(), 12, partition_inverse=partition, dist_min=129)]
         out[rank] = res
     finally:
         dist.destroy_process_group()
@@ -89,3 +89,71 @@ def test_partial_inverse_columns(n, c0, c1):
     np.testing.assert_allclose(Mp[sel], Mf[sel], rtol=1e-10, atol=1e-12 * np.abs(Mf[sel]).max())
     up = ~lo
     np.testing.assert_array_equal(Mp[up], S[up])
+
+
+def _chol_worker(rank, world, port, n, dist_min, out):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vgposp_amd import linalg
+        from vgposp_amd._lib import query
+        from vgposp_amd.dist_cholesky import DistCholesky, HipCholeskyOps
+        torch.cuda.set_device(0)
+        X = np.random.default_rng(11).uniform(-2, 2, (n, 3))
+        S = ogp.kernel_matrix("eq", X, X, 1.0, 0.6)[0] + 0.02 * np.eye(n)
+        A = torch.as_tensor(S, device="cuda")
+        ws = linalg.workspace(query("vgposp_potrf_workspace_bytes", n))
+        info = torch.zeros(1, dtype=torch.int32, device="cuda")
+        dc = DistCholesky(HipCholeskyOps(A, ws.data_ptr(), ws.numel(), info), dist_min=dist_min)
+        dc.factor()
+        torch.cuda.synchronize()
+        out[rank] = (A.cpu().numpy(), int(info.item()), dc.exchanged)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,dist_min", [(2, 3000, 1024), (3, 2200, 600), (2, 1300, 129)])
+def test_dist_cholesky_on_gpu(world, n, dist_min):
+    """DistCholesky over HIP pieces (ranks share cuda:0, gloo staging): every rank ends with the
+    single-GPU factor (vgposp_potrf_lower) to rounding, the upper triangle untouched."""
+    import torch
+    from vgposp_amd import linalg
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_chol_worker, args=(world, _free_port(), n, dist_min, out), nprocs=world, join=True)
+    X = np.random.default_rng(11).uniform(-2, 2, (n, 3))
+    S = ogp.kernel_matrix("eq", X, X, 1.0, 0.6)[0] + 0.02 * np.eye(n)
+    ref, _, _ = linalg.cholesky_(torch.as_tensor(S, device="cuda")[None].clone(), invert=False)
+    ref = ref[0].cpu().numpy()
+    lo = np.tril(np.ones((n, n), dtype=bool))
+    for r in range(world):
+        A, info, ex = out[r]
+        assert info == 0 and ex > 0
+        np.testing.assert_allclose(A[lo], ref[lo], rtol=1e-11, atol=1e-13)
+        np.testing.assert_array_equal(A[~lo], S[~lo])
+
+
+@pytest.mark.parametrize("lower", [0, 1])
+def test_pack_rows_round_trip(lower):
+    import torch
+    from vgposp_amd._lib import call, query
+    from vgposp_amd.linalg import _p
+    n = 900
+    A = torch.rand(n, n, dtype=torch.float64, device="cuda")
+    r0, r1, c0 = 300, 700, (200 if lower else 50)
+    c1 = 700 if lower else 650
+    m = query("vgposp_pack_elems", r0, r1, c0, c1, lower)
+    buf = torch.empty(m, dtype=torch.float64, device="cuda")
+    call("vgposp_pack_rows", _p(A), n, r0, r1, c0, c1, lower, _p(buf), 0, None)
+    B = torch.zeros_like(A)
+    call("vgposp_pack_rows", _p(B), n, r0, r1, c0, c1, lower, _p(buf), 1, None)
+    torch.cuda.synchronize()
+    a, b = A.cpu().numpy(), B.cpu().numpy()
+    mask = np.zeros((n, n), dtype=bool)
+    for r in range(r0, r1):
+        mask[r, c0:(r + 1 if lower else c1)] = True
+    assert m == mask.sum()
+    np.testing.assert_array_equal(b[mask], a[mask])
+    assert not b[~mask].any()

@@ -24,7 +24,63 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, names, lazy, out, partition=False):
+def _grid_cov():
+    from oracle import gp as ogp
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    X = grid_points((12, 10, 9), jitter=0.05, seed=0)
+    return ogp.kernel_matrix("eq", X, X, 1.0, 2 * grid_spacing((12, 10, 9)))[0] + 0.010001 * np.eye(len(X))
+
+
+def _chol_worker(rank, world, port, n, dist_min, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.numpy_greedy_backend import NumpyCholeskyOps
+        from vgposp_amd.dist_cholesky import DistCholesky
+        X = np.random.default_rng(5).uniform(-2, 2, (n, 3))
+        S = np.exp(-0.5 * ((X[:, None] - X[None]) ** 2).sum(-1) / 0.6 ** 2) + 0.05 * np.eye(n)
+        A = S.copy()
+        dc = DistCholesky(NumpyCholeskyOps(A), dist_min=dist_min)
+        dc.factor()
+        out[rank] = (A, S, dc.exchanged)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,dist_min", [(2, 700, 129), (3, 700, 129), (3, 1000, 400),
+                                              (4, 520, 129)])
+def test_dist_cholesky_gloo(world, n, dist_min):
+    """DistCholesky: each rank solves its share of every large node's panel and SYRK band; after
+    the all-gathers every rank holds the full factor (the upper triangle keeps Sigma)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_chol_worker, args=(world, _free_port(), n, dist_min, out), nprocs=world, join=True)
+    A0, S, ex = out[0]
+    L = np.linalg.cholesky(S)
+    lo = np.tril(np.ones((n, n), dtype=bool))
+    assert ex > 0
+    for r in range(world):
+        A = out[r][0]
+        np.testing.assert_allclose(A[lo], L[lo], rtol=1e-10, atol=1e-12)
+        np.testing.assert_array_equal(A[~lo], S[~lo])
+
+
+def test_share_bounds():
+    from vgposp_amd.dist_cholesky import even_rows, lower_bands
+    for n in (4096, 32768, 1000):
+        for world in (1, 2, 3, 8):
+            for f in (even_rows, lower_bands):
+                e = f(n, world)
+                assert e[0][0] == 0 and e[-1][1] == n
+                assert all(a <= b for a, b in e)
+                assert all(a % 128 == 0 for a, _ in e)
+    bands = lower_bands(32768, 8)
+    area = [b * (b + 1) / 2 - a * (a + 1) / 2 for a, b in bands]
+    assert max(area) / min(area) < 1.1  # 128-row granularity
+
+
+def _worker(rank, world, port, names, lazy, out, partition=False, dist_min=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -33,10 +89,10 @@ def _worker(rank, world, port, names, lazy, out, partition=False):
         from vgposp_amd.sharded_placement import ShardedGreedyPlacement
         res = {}
         for name in names:
-            e = CASES[name]
-            cov = placement_cov(name, e)
+            e = {"k": 12} if name == "grid1080" else CASES[name]
+            cov = _grid_cov() if name == "grid1080" else placement_cov(name, e)
             sh = ShardedGreedyPlacement(NumpyGreedyBackend(cov, e["k"]), partition_inverse=partition,
-                                        align=4)
+                                        align=4, dist_min=dist_min)
             A, _, _ = sh.run(e["k"], lazy=lazy)
             res[name] = [int(a) for a in A]
         out[rank] = res
@@ -55,6 +111,20 @@ def test_sharded_matches_reference(world, lazy):
         for name in names:
             exp = CASES[name]["alg2" if lazy else "alg1"]
             assert out[r][name] == exp, (r, name)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_dist_factor_matches_reference(world):
+    """Partitioned inverse on a factor the ranks computed together (DistCholesky, every node above
+    128 split): same picks as the precision oracle on a 1,080-point grid."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), ["grid1080", "spd40"], True, out, True, 129),
+             nprocs=world, join=True)
+    exp = [int(a) for a in op.placement_lazy_precision(_grid_cov(), 12)]
+    for r in range(world):
+        assert out[r]["grid1080"] == exp, r
+        assert out[r]["spd40"] == CASES["spd40"]["alg2"], r
 
 
 @pytest.mark.parametrize("world", [2, 3])

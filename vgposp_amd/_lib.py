@@ -118,6 +118,22 @@ SIGNATURES = {
                                      _c_void_p, _size, _c_void_p]),
     "vgposp_greedy_update_ex": (_i32, [_c_void_p, _i64, _i64, _i32, _i32, _i64, _i64, _c_void_p,
                                        _i32, _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_prepare": (_i32, [_c_void_p, _i64, _i64, _i32, _f64, _f64, _f64, _c_void_p,
+                                     _c_void_p, _size, _c_void_p]),
+    "vgposp_greedy_fact_ws": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p),
+                                     ctypes.POINTER(_size)]),
+    "vgposp_greedy_finish_slab": (_i32, [_c_void_p, _i64, _i64, _i32, _i64, _i64, _c_void_p,
+                                         _size, _c_void_p, _size, _c_void_p]),
+    "vgposp_potrf_split": (_i64, [_i64]),
+    "vgposp_potrf_block": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p, _size,
+                                  _c_void_p]),
+    "vgposp_potrf_panel": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _i64, _c_void_p, _size,
+                                  _c_void_p]),
+    "vgposp_potrf_trailing": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _i64, _c_void_p,
+                                     _size, _c_void_p]),
+    "vgposp_pack_elems": (_i64, [_i64, _i64, _i64, _i64, _i32]),
+    "vgposp_pack_rows": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _i32, _c_void_p, _i32,
+                                _c_void_p]),
     "vgposp_greedy_xcol": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p)]),
     "vgposp_greedy_buffers": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p),
                                      ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64)]),

@@ -575,39 +575,77 @@ extern "C" size_t vgposp_greedy_slab_tmp_bytes(int64_t n, int64_t c0, int64_t c1
   return partial_inverse_tmp_bytes(n, c0, c1);
 }
 
-extern "C" int vgposp_greedy_init_slab(double* Sigma, int64_t n, int64_t lda, int kmax,
-                                       double jitter, double threshold, double cache_init,
-                                       int64_t c0, int64_t c1, double* tmp, size_t tmp_bytes,
-                                       int* info, void* ws, size_t ws_bytes, void* stream) {
-  clear_error();
-  VG_CHECK_ARG(Sigma != nullptr, 1);
-  VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
-  VG_CHECK_ARG(lda >= n, 3);
-  VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
-  VG_CHECK_ARG(jitter >= 0.0 && jitter < 1e300, 5);
-  VG_CHECK_ARG(threshold >= 0.0, 6);
-  VG_CHECK_ARG(cache_init == cache_init, 7);
-  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c0 % 128 == 0, 8);
-  VG_CHECK_ARG(c1 <= n && (c1 % 128 == 0 || c1 == n), 9);
-  VG_CHECK_ARG(c1 == c0 || (tmp != nullptr && tmp_bytes >= partial_inverse_tmp_bytes(n, c0, c1)),
-               10);
-  VG_CHECK_ARG(info != nullptr, 12);
-  VG_CHECK_ARG(ws != nullptr, 13);
-  GreedyWS w = greedy_layout(ws, n, kmax);
-  if (ws_bytes < w.bytes) {
-    set_error("vgposp_greedy_init_slab: workspace %zu < %zu bytes", ws_bytes, w.bytes);
+static int check_prepare(const char* fn, double* Sigma, int64_t n, int64_t lda, int kmax,
+                         double jitter, double threshold, double cache_init, int* info, void* ws,
+                         size_t ws_bytes, GreedyWS* w) {
+  if (Sigma == nullptr) { set_error("%s: bad argument 1", fn); return -1; }
+  if (!(n >= 1 && n <= (int64_t)MAXCH * CH)) { set_error("%s: bad argument 2", fn); return -2; }
+  if (lda < n) { set_error("%s: bad argument 3", fn); return -3; }
+  if (!(kmax >= 1 && kmax <= n)) { set_error("%s: bad argument 4", fn); return -4; }
+  if (!(jitter >= 0.0 && jitter < 1e300)) { set_error("%s: bad argument 5", fn); return -5; }
+  if (!(threshold >= 0.0)) { set_error("%s: bad argument 6", fn); return -6; }
+  if (cache_init != cache_init) { set_error("%s: bad argument 7", fn); return -7; }
+  if (info == nullptr) { set_error("%s: info is null", fn); return -8; }
+  if (ws == nullptr) { set_error("%s: workspace is null", fn); return VGPOSP_E_WS; }
+  *w = greedy_layout(ws, n, kmax);
+  if (ws_bytes < w->bytes) {
+    set_error("%s: workspace %zu < %zu bytes", fn, ws_bytes, w->bytes);
     return VGPOSP_E_WS;
   }
+  return 0;
+}
+
+extern "C" int vgposp_greedy_prepare(double* Sigma, int64_t n, int64_t lda, int kmax,
+                                     double jitter, double threshold, double cache_init, int* info,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  GreedyWS w;
+  if (int rc = check_prepare(__func__, Sigma, n, lda, kmax, jitter, threshold, cache_init, info,
+                             ws, ws_bytes, &w))
+    return rc;
   hipStream_t s = as_stream(stream);
   VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
                      n, lda, jitter, threshold, cache_init, w);
   VG_LAUNCH_CHECK();
-  void* fws = greedy_fact_ws(ws, w, n);
-  int rc = potrf_one(Sigma, n, lda, /*invert=*/0, nullptr, info, fws, s);
-  if (rc) return rc;
+  return 0;
+}
+
+extern "C" int vgposp_greedy_fact_ws(void* ws, int64_t n, int kmax, void** fws,
+                                     size_t* fws_bytes) {
+  clear_error();
+  VG_CHECK_ARG(ws != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(kmax >= 1, 3);
+  VG_CHECK_ARG(fws != nullptr && fws_bytes != nullptr, 4);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  *fws = greedy_fact_ws(ws, w, n);
+  *fws_bytes = potrf_ws_bytes(n);
+  return 0;
+}
+
+extern "C" int vgposp_greedy_finish_slab(double* Sigma, int64_t n, int64_t lda, int kmax,
+                                         int64_t c0, int64_t c1, double* tmp, size_t tmp_bytes,
+                                         void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(Sigma != nullptr, 1);
+  VG_CHECK_ARG(n >= 1 && n <= (int64_t)MAXCH * CH, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(kmax >= 1 && kmax <= n, 4);
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c0 % 128 == 0, 5);
+  VG_CHECK_ARG(c1 <= n && (c1 % 128 == 0 || c1 == n), 6);
+  VG_CHECK_ARG(c1 == c0 || (tmp != nullptr && tmp_bytes >= partial_inverse_tmp_bytes(n, c0, c1)),
+               7);
+  VG_CHECK_ARG(ws != nullptr, 9);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  if (ws_bytes < w.bytes) {
+    set_error("vgposp_greedy_finish_slab: workspace %zu < %zu bytes", ws_bytes, w.bytes);
+    return VGPOSP_E_WS;
+  }
   if (c1 == c0) return 0;
-  if ((rc = partial_inverse(Sigma, n, lda, c0, c1, tmp, fws, s))) return rc;
+  hipStream_t s = as_stream(stream);
+  int rc = partial_inverse(Sigma, n, lda, c0, c1, tmp, greedy_fact_ws(ws, w, n), s);
+  if (rc) return rc;
   // Q_ii = |M e_i|^2 for the slab's columns -> part (reduced in the round-0 update)
   dim3 g((unsigned)ceil_div(c1 - (c0 & ~(int64_t)1), TRMV_COLS), (unsigned)ceil_div(n, RC));
   const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);
@@ -616,6 +654,26 @@ extern "C" int vgposp_greedy_init_slab(double* Sigma, int64_t n, int64_t lda, in
                      nullptr, w.part, c0, c1, vec);
   VG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int vgposp_greedy_init_slab(double* Sigma, int64_t n, int64_t lda, int kmax,
+                                       double jitter, double threshold, double cache_init,
+                                       int64_t c0, int64_t c1, double* tmp, size_t tmp_bytes,
+                                       int* info, void* ws, size_t ws_bytes, void* stream) {
+  clear_error();
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c0 % 128 == 0, 8);
+  VG_CHECK_ARG(c1 <= n && (c1 % 128 == 0 || c1 == n), 9);
+  VG_CHECK_ARG(c1 == c0 || (tmp != nullptr && tmp_bytes >= partial_inverse_tmp_bytes(n, c0, c1)),
+               10);
+  int rc = vgposp_greedy_prepare(Sigma, n, lda, kmax, jitter, threshold, cache_init, info, ws,
+                                 ws_bytes, stream);
+  if (rc) return rc;
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  if ((rc = potrf_one(Sigma, n, lda, /*invert=*/0, nullptr, info, greedy_fact_ws(ws, w, n),
+                      as_stream(stream))))
+    return rc;
+  return vgposp_greedy_finish_slab(Sigma, n, lda, kmax, c0, c1, tmp, tmp_bytes, ws, ws_bytes,
+                                   stream);
 }
 
 extern "C" int vgposp_greedy_xcol(void* ws, int64_t n, int kmax, double** xcol) {

@@ -517,6 +517,89 @@ int partial_inverse(double* A, int64_t n, int64_t lda, int64_t c0, int64_t c1, d
 }
 
 // ---------------------------------------------------------------------------------------------
+// Pieces of a Cholesky distributed over R ranks that each hold the whole matrix (the host mirrors
+// potrf_rec's splits, vgposp_amd/dist_cholesky.py).  ws is a potrf workspace for the WHOLE n, so the
+// leaf / block inverses of every diagonal block sit at their global columns, exactly where the
+// single-GPU recursion leaves them (partial_inverse and trsm_rec read them from there).
+// ---------------------------------------------------------------------------------------------
+
+// The diagonal block [col0, col0 + nb) factored in place by the single-GPU recursion.
+int potrf_block(double* A, int64_t n, int64_t lda, int64_t col0, int64_t nb, int* info, void* ws,
+                hipStream_t s) {
+  if (int rc = ensure_leaf_attr()) return rc;
+  Fact f = make_fact(n, lda, ws, nullptr, info, s);
+  return potrf_rec(f, A + col0 * (lda + 1), nb, col0, n > NBI);
+}
+
+// Node (col0, nsub) split at n1: rows [r0, r1) of its panel (global rows col0 + n1 + r0 ...)
+//   A21 <- A21 L11^-T
+int potrf_panel(double* A, int64_t n, int64_t lda, int64_t col0, int64_t n1, int64_t r0,
+                int64_t r1, void* ws, hipStream_t s) {
+  Fact f = make_fact(n, lda, ws, nullptr, nullptr, s);
+  double* A11 = A + col0 * (lda + 1);
+  return trsm_rec(f, A11 + (n1 + r0) * lda, r1 - r0, lda, A11, n1, col0, n > NBI);
+}
+
+// Node (col0, nsub) split at n1, n2 = nsub - n1: rows [b0, b1) of the lower triangle of A22
+//   A22 -= L21 L21^T   (the rectangle left of the band's diagonal square, then the square)
+int potrf_trailing(double* A, int64_t n, int64_t lda, int64_t col0, int64_t n1, int64_t b0,
+                   int64_t b1, void* ws, hipStream_t s) {
+  Fact f = make_fact(n, lda, ws, nullptr, nullptr, s);
+  double* L21 = A + (col0 + n1) * lda + col0;
+  double* A22 = L21 + n1;
+  const int64_t m = b1 - b0;
+  int rc;
+  if (m <= 0) return 0;
+  if (b0 > 0 && (rc = pgemm(f, 0, 1, m, b0, n1, -1.0, L21 + b0 * lda, lda, L21, lda, 1.0,
+                            A22 + b0 * lda, lda, VGPOSP_FULL, 0, 0)))
+    return rc;
+  return pgemm(f, 0, 1, m, m, n1, -1.0, L21 + b0 * lda, lda, L21 + b0 * lda, lda, 1.0,
+               A22 + b0 * lda + b0, lda, VGPOSP_LOWER, 0, 0);
+}
+
+// Row block <-> contiguous buffer, for the all-gathers between the pieces above.  Rows [r0, r1),
+// columns [c0, c1) (lower = 0), or the lower trapezoid: columns [c0, r] of row r (lower = 1,
+// c0 <= r0 and c1 >= r1), packed row after row.
+__global__ void pack_lower_kernel(double* A, int64_t lda, int64_t r0, int64_t c0, double* buf,
+                                  int unpack) {
+  const int64_t i = blockIdx.x, r = r0 + i;
+  const int64_t len = r + 1 - c0;
+  const int64_t off = i * (r0 + 1 - c0) + i * (i - 1) / 2;
+  double* row = A + r * lda + c0;
+  for (int64_t c = threadIdx.x; c < len; c += blockDim.x) {
+    if (unpack) row[c] = buf[off + c];
+    else buf[off + c] = row[c];
+  }
+}
+
+int64_t pack_elems(int64_t r0, int64_t r1, int64_t c0, int64_t c1, int lower) {
+  const int64_t m = r1 - r0;
+  if (m <= 0) return 0;
+  if (!lower) return m * (c1 - c0);
+  return m * (r0 + 1 - c0) + m * (m - 1) / 2;
+}
+
+int pack_rows(double* A, int64_t lda, int64_t r0, int64_t r1, int64_t c0, int64_t c1, int lower,
+              double* buf, int unpack, hipStream_t s) {
+  const int64_t m = r1 - r0;
+  if (m <= 0) return 0;
+  if (!lower) {
+    const size_t w = (size_t)(c1 - c0) * sizeof(double);
+    if (unpack)
+      VG_HIP(hipMemcpy2DAsync(A + r0 * lda + c0, lda * sizeof(double), buf, w, w, m,
+                              hipMemcpyDeviceToDevice, s));
+    else
+      VG_HIP(hipMemcpy2DAsync(buf, w, A + r0 * lda + c0, lda * sizeof(double), w, m,
+                              hipMemcpyDeviceToDevice, s));
+    return 0;
+  }
+  hipLaunchKernelGGL(pack_lower_kernel, dim3((unsigned)m), dim3(256), 0, s, A, lda, r0, c0, buf,
+                     unpack);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Left-side triangular solve with a factor from vgposp_potrf_lower(invert = 0):
 //   B (n x m) <- L^-1 B (trans = 0, forward)  or  L^-T B (trans = 1, backward)
 // Recursion on the same splits as potrf_rec: the off-diagonal part is one GEMM per level
@@ -650,4 +733,88 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
     if (rc) return rc;
   }
   return 0;
+}
+
+extern "C" int64_t vgposp_potrf_split(int64_t n) {
+  return n > vgposp::NB ? vgposp::split_point(n) : 0;
+}
+
+extern "C" int vgposp_potrf_block(double* A, int64_t n, int64_t lda, int64_t col0, int64_t nb,
+                                  int* info, void* ws, size_t ws_bytes, void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(A != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(col0 >= 0 && col0 % NB == 0, 4);
+  VG_CHECK_ARG(nb >= 1 && col0 + nb <= n, 5);
+  VG_CHECK_ARG(info != nullptr, 6);
+  VG_CHECK_ARG(ws != nullptr, 7);
+  if (ws_bytes < potrf_ws_bytes(n)) {
+    set_error("vgposp_potrf_block: workspace %zu < %zu bytes", ws_bytes, potrf_ws_bytes(n));
+    return VGPOSP_E_WS;
+  }
+  return potrf_block(A, n, lda, col0, nb, info, ws, as_stream(stream));
+}
+
+extern "C" int vgposp_potrf_panel(double* A, int64_t n, int64_t lda, int64_t col0, int64_t nsub,
+                                  int64_t r0, int64_t r1, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(A != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(col0 >= 0 && col0 % NB == 0, 4);
+  VG_CHECK_ARG(nsub > NBI && col0 + nsub <= n, 5);  // smaller nodes: vgposp_potrf_block
+  const int64_t n1 = split_point(nsub);
+  VG_CHECK_ARG(r0 >= 0 && r0 <= r1, 6);
+  VG_CHECK_ARG(r1 <= nsub - n1, 7);
+  VG_CHECK_ARG(ws != nullptr, 8);
+  if (ws_bytes < potrf_ws_bytes(n)) {
+    set_error("vgposp_potrf_panel: workspace %zu < %zu bytes", ws_bytes, potrf_ws_bytes(n));
+    return VGPOSP_E_WS;
+  }
+  if (r1 == r0) return 0;
+  return potrf_panel(A, n, lda, col0, n1, r0, r1, ws, as_stream(stream));
+}
+
+extern "C" int vgposp_potrf_trailing(double* A, int64_t n, int64_t lda, int64_t col0,
+                                     int64_t nsub, int64_t b0, int64_t b1, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(A != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(lda >= n, 3);
+  VG_CHECK_ARG(col0 >= 0 && col0 % NB == 0, 4);
+  VG_CHECK_ARG(nsub > NBI && col0 + nsub <= n, 5);
+  const int64_t n1 = split_point(nsub);
+  VG_CHECK_ARG(b0 >= 0 && b0 <= b1, 6);
+  VG_CHECK_ARG(b1 <= nsub - n1, 7);
+  VG_CHECK_ARG(ws != nullptr, 8);
+  if (ws_bytes < potrf_ws_bytes(n)) {
+    set_error("vgposp_potrf_trailing: workspace %zu < %zu bytes", ws_bytes, potrf_ws_bytes(n));
+    return VGPOSP_E_WS;
+  }
+  return potrf_trailing(A, n, lda, col0, n1, b0, b1, ws, as_stream(stream));
+}
+
+extern "C" int64_t vgposp_pack_elems(int64_t r0, int64_t r1, int64_t c0, int64_t c1, int lower) {
+  if (r0 < 0 || c0 < 0 || r1 < r0 || c1 < c0) return -1;
+  if (lower && (c0 > r0 || c1 < r1)) return -1;
+  return vgposp::pack_elems(r0, r1, c0, c1, lower);
+}
+
+extern "C" int vgposp_pack_rows(double* A, int64_t lda, int64_t r0, int64_t r1, int64_t c0,
+                                int64_t c1, int lower, double* buf, int unpack, void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(A != nullptr || r1 == r0, 1);
+  VG_CHECK_ARG(lda >= c1, 2);
+  VG_CHECK_ARG(r0 >= 0 && r0 <= r1, 3);
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1, 5);
+  VG_CHECK_ARG(lower == 0 || (lower == 1 && c0 <= r0 && c1 >= r1), 7);
+  VG_CHECK_ARG(buf != nullptr || r1 == r0, 8);
+  return pack_rows(A, lda, r0, r1, c0, c1, lower, buf, unpack, as_stream(stream));
 }

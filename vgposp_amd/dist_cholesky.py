@@ -1,0 +1,170 @@
+"""Cholesky of ONE covariance over R ranks (one process per GPU) that each hold it whole.
+
+The candidate-sharded placement (``sharded_placement.py``) needs the lower factor L
+of Sigma on every rank before each rank forms its slab's columns of L^-1.  The factorization is the
+O(N^3) step behind the reference's pinv calls (placement_algorithm2.py:399-413); replicated, it
+bounds the speed-up of one 65k problem on 8 GPUs at ~2x.  Here the ranks split it:
+
+* the host walks ``vgposp_potrf_lower``'s own recursion (split points from ``vgposp_potrf_split``),
+  so every diagonal block, leaf inverse and 512-block inverse is the single-GPU one and lands at
+  its global column of the potrf workspace (where ``vgposp_greedy_finish_slab`` reads them);
+* a node smaller than ``dist_min`` (or of at most 512 columns, whose inverse the recursion forms
+  as a block) is factored whole on every rank (``vgposp_potrf_block``: the latency-bound chain of
+  leaves, ~2 % of the flops);
+* a larger node (col0, nsub), split at n1, n2 = nsub - n1, after its top-left child:
+    1. panel TRSM L21 = A21 L11^-T: rank r solves an even share of L21's n2 rows
+       (``vgposp_potrf_panel``); the shares are all-gathered (n2 x n1 doubles in total);
+    2. SYRK A22 -= L21 L21^T (lower): rank r updates a band of A22's rows balanced by lower-triangle
+       area (``vgposp_potrf_trailing``); the bands' lower trapezoids are all-gathered
+       (n2 (n2 + 1) / 2 doubles in total);
+  then its bottom-right child.
+
+Every rank ends with the same L (the upper triangle of the buffer, Sigma, is never written).  The
+all-gathers run on RCCL over device buffers ("nccl" backend), or through host staging on gloo (the
+CPU tests and the 2-ranks-on-one-GPU test).  At N = 65,536 and R = 8 they move ~26 GB in total
+(each rank receives 7/8 of it); the flops per rank drop ~7x.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+import torch.distributed as dist
+
+from ._lib import call, query
+from .linalg import _p, _stream
+
+DIST_MIN = 4096   # nodes at least this large are split over the ranks
+BLOCK_INV = 512   # nodes up to this size are factored whole: the recursion inverts them as blocks
+ALIGN = 128       # share boundaries on GEMM-tile rows
+
+
+def even_rows(n, world, align=ALIGN):
+    """[a, b) row shares of n rows, equal up to ``align``."""
+    edges = [0]
+    for r in range(1, world):
+        e = int(round(n * r / world / align)) * align
+        edges.append(min(max(e, edges[-1]), n))
+    edges.append(n)
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
+def lower_bands(n, world, align=ALIGN):
+    """[a, b) row bands of an n x n lower triangle with equal area: edge r at n sqrt(r / world)."""
+    edges = [0]
+    for r in range(1, world):
+        e = int(round(n * math.sqrt(r / world) / align)) * align
+        edges.append(min(max(e, edges[-1]), n))
+    edges.append(n)
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
+class HipCholeskyOps:
+    """The device pieces (libvgposp) on an [n, n] fp64 tensor with a potrf workspace for n."""
+
+    def __init__(self, A, fws_ptr, fws_bytes, info):
+        self.A = A
+        self.n = int(A.shape[0])
+        self.lda = int(A.stride(0))
+        self.fws = fws_ptr
+        self.fws_bytes = int(fws_bytes)
+        self.info = info
+        self.device = A.device
+
+    def split(self, n):
+        return query("vgposp_potrf_split", n)
+
+    def block(self, col0, nb):
+        call("vgposp_potrf_block", _p(self.A), self.n, self.lda, col0, nb, _p(self.info),
+             self.fws, self.fws_bytes, _stream())
+
+    def panel(self, col0, nsub, r0, r1):
+        call("vgposp_potrf_panel", _p(self.A), self.n, self.lda, col0, nsub, r0, r1, self.fws,
+             self.fws_bytes, _stream())
+
+    def trailing(self, col0, nsub, b0, b1):
+        call("vgposp_potrf_trailing", _p(self.A), self.n, self.lda, col0, nsub, b0, b1, self.fws,
+             self.fws_bytes, _stream())
+
+    def pack_elems(self, r0, r1, c0, c1, lower):
+        return query("vgposp_pack_elems", r0, r1, c0, c1, int(lower))
+
+    def pack(self, r0, r1, c0, c1, lower, buf, unpack):
+        call("vgposp_pack_rows", _p(self.A), self.lda, r0, r1, c0, c1, int(lower), _p(buf),
+             int(unpack), _stream())
+
+
+class DistCholesky:
+    """Factor ``ops``'s matrix (lower, in place) with the work of every large recursion node split
+    over the ranks of ``group``."""
+
+    def __init__(self, ops, group=None, dist_min=DIST_MIN):
+        self.ops = ops
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.dist_min = int(dist_min)
+        dev = ops.device
+        self.staging = (self.world > 1 and dist.get_backend(group) == "gloo"
+                        and dev.type != "cpu")
+        self._bufs = {}
+        self.exchanged = 0  # doubles all-gathered (diagnostic)
+
+    def factor(self):
+        self._rec(0, self.ops.n)
+
+    def _rec(self, col0, nsub):
+        ops = self.ops
+        if self.world == 1 or nsub < self.dist_min or nsub <= BLOCK_INV:
+            ops.block(col0, nsub)
+            return
+        n1 = ops.split(nsub)
+        n2 = nsub - n1
+        base = col0 + n1
+        self._rec(col0, n1)
+        shares = even_rows(n2, self.world)
+        ops.panel(col0, nsub, *shares[self.rank])
+        self._exchange([(base + a, base + b, col0, base, 0) for a, b in shares])
+        bands = lower_bands(n2, self.world)
+        ops.trailing(col0, nsub, *bands[self.rank])
+        self._exchange([(base + a, base + b, base, base + b, 1) for a, b in bands])
+        self._rec(base, n2)
+
+    def _buf(self, key, numel, device):
+        b = self._bufs.get(key)
+        if b is None or b.numel() < numel:
+            b = torch.empty(numel, dtype=torch.float64, device=device)
+            self._bufs[key] = b
+        return b[:numel]
+
+    def _exchange(self, pieces):
+        """All-gather every rank's piece (r0, r1, c0, c1, lower) of the matrix."""
+        ops = self.ops
+        sizes = [ops.pack_elems(*p) for p in pieces]
+        S = max(sizes)
+        if S == 0:
+            return
+        send = self._buf("send", S, ops.device)
+        recv = self._buf("recv", self.world * S, ops.device)
+        if sizes[self.rank]:
+            ops.pack(*pieces[self.rank], send, False)
+        if self.staging:
+            hs = send.cpu()
+            hr = torch.empty(self.world * S, dtype=torch.float64)
+            dist.all_gather_into_tensor(hr, hs, group=self.group)
+            recv.copy_(hr)
+        else:
+            dist.all_gather_into_tensor(recv, send, group=self.group)
+        for r, p in enumerate(pieces):
+            if r != self.rank and sizes[r]:
+                ops.pack(*p, recv[r * S:r * S + sizes[r]], True)
+        self.exchanged += sum(sizes)
+
+
+def greedy_cholesky_ops(g):
+    """HipCholeskyOps over a GreedyPlacement's Sigma and the potrf workspace inside its greedy
+    workspace (so vgposp_greedy_finish_slab finds the leaf / block inverses)."""
+    fws, fbytes = ctypes.c_void_p(), ctypes.c_size_t()
+    call("vgposp_greedy_fact_ws", _p(g.ws), g.n, g.kmax, ctypes.byref(fws), ctypes.byref(fbytes))
+    return HipCholeskyOps(g.S, fws.value, fbytes.value, g.info)

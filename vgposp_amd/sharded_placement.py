@@ -1,11 +1,13 @@
 """Candidate-sharded greedy MI placement across GPUs, one process per GPU.
 
-The candidate set V is cut into R contiguous slabs.  Every rank factors the covariance (the
-O(N^3) Cholesky is replicated — "replicas only" for the factorization at N <= 65k).
-With ``partition_inverse=True`` (what bench.py runs) a rank then forms L^-1 only in its own slab's
-columns (vgposp_greedy_init_slab: about 1/R of the inverse's flops, slabs balanced by that work,
-128-aligned); otherwise the fused Cholesky + full inverse is replicated and the slabs balance the
-triangular mat-vec (column c of L^-1 has n - c stored rows).  Per round:
+The candidate set V is cut into R contiguous slabs.  With ``partition_inverse=True`` (what
+bench.py runs) the ranks factor the covariance TOGETHER (``dist_cholesky.DistCholesky``: every large
+node of the recursive Cholesky has its panel TRSM and trailing SYRK split over the ranks, the
+shares all-gathered; ``dist_factor=False`` replicates the factorization instead) and each rank then
+forms L^-1 only in its own slab's columns (vgposp_greedy_finish_slab: about 1/R of the inverse's
+flops, slabs balanced by that work, 128-aligned).  With ``partition_inverse=False`` the fused
+Cholesky + full inverse is replicated and the slabs balance the triangular mat-vec (column c of
+L^-1 has n - c stored rows).  Per round:
 
   0. (partitioned inverse) the owner of the last pick's column of L^-1 writes it, the others zeros,
      and ONE sum-all-reduce of that column (N x 8 bytes) gives every rank the mat-vec's vector;
@@ -97,6 +99,27 @@ class HipGreedyBackend:
              _p(self._tmp), self._tmp.numel(), _p(g.info), _p(g.ws), g.ws.numel(), _stream())
         g.rounds = 0
 
+    def prepare(self):
+        """vgposp_greedy_prepare: the init kernel only (the caller factors Sigma)."""
+        g = self.g
+        call("vgposp_greedy_prepare", _p(g.S), g.n, g.S.stride(0), g.kmax, *g.params, _p(g.info),
+             _p(g.ws), g.ws.numel(), _stream())
+        g.rounds = 0
+
+    def chol_ops(self):
+        from .dist_cholesky import greedy_cholesky_ops
+        return greedy_cholesky_ops(self.g)
+
+    def finish_slab(self, c0, c1):
+        """After the factorization: L^-1 in columns [c0, c1) and their column norms."""
+        from ._lib import query
+        g = self.g
+        need = query("vgposp_greedy_slab_tmp_bytes", g.n, c0, c1)
+        if self._tmp is None or self._tmp.numel() < need:
+            self._tmp = torch.empty(max(need, 8), dtype=torch.uint8, device=g.S.device)
+        call("vgposp_greedy_finish_slab", _p(g.S), g.n, g.S.stride(0), g.kmax, c0, c1,
+             _p(self._tmp), self._tmp.numel(), _p(g.ws), g.ws.numel(), _stream())
+
     def extract(self, rnd, own0, own1):
         g = self.g
         call("vgposp_greedy_extract", _p(g.S), g.n, g.S.stride(0), g.kmax, rnd, own0, own1,
@@ -127,8 +150,11 @@ class HipGreedyBackend:
 
 
 class ShardedGreedyPlacement:
-    def __init__(self, backend, group=None, balance=True, partition_inverse=False, align=128):
+    def __init__(self, backend, group=None, balance=True, partition_inverse=False, align=128,
+                 dist_factor=True, dist_min=None):
         self.b = backend
+        self.dist_factor = bool(dist_factor)
+        self.dist_min = dist_min
         self.group = group
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -182,7 +208,14 @@ class ShardedGreedyPlacement:
             dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group)
 
     def run(self, k, lazy=True):
-        if self.partition:
+        if self.partition and self.world > 1 and self.dist_factor:
+            from .dist_cholesky import DIST_MIN, DistCholesky
+            self.b.prepare()
+            dc = DistCholesky(self.b.chol_ops(), self.group,
+                              DIST_MIN if self.dist_min is None else self.dist_min)
+            dc.factor()
+            self.b.finish_slab(self.c0, self.c1)
+        elif self.partition:
             self.b.init_slab(self.c0, self.c1)
         else:
             self.b.init()
@@ -199,9 +232,11 @@ class ShardedGreedyPlacement:
         return self.b.result()
 
 
-def placement_algorithm_2_sharded(cov_vv, k, group=None, lazy=True, partition_inverse=True):
+def placement_algorithm_2_sharded(cov_vv, k, group=None, lazy=True, partition_inverse=True,
+                                  dist_factor=True, dist_min=None):
     """placement_algorithm_2 with candidates sharded over the ranks of ``group`` (every rank
     passes the same cov_vv and gets the same list)."""
     sh = ShardedGreedyPlacement(HipGreedyBackend(cov_vv, k, copy=True), group,
-                                partition_inverse=partition_inverse)
+                                partition_inverse=partition_inverse, dist_factor=dist_factor,
+                                dist_min=dist_min)
     return sh.run(k, lazy)[0]
