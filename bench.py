@@ -158,7 +158,7 @@ def load_traffic(path, kernel, N, shape, k):
     return {"bytes_per_launch": kern["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
 
 
-def vgp_line(args, which="c3"):
+def vgp_line(args, which="c3", precision="fp64"):
     """Config C3 or C5: VGP training steps/s on this GPU — optimal posterior over all
     N + minibatch ELBO + analytic gradient + Adam(0.01), minibatch N / 8.
       C3: N = 64^3 observations over [-7, 7]^3, M = 8^3, 3-D.
@@ -171,7 +171,7 @@ def vgp_line(args, which="c3"):
     X, y, Z = vgp_c3_data() if which == "c3" else vgp_c5_data()
     N, M = len(X), len(Z)
     B = N // 8
-    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B)
+    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B, precision=precision)
     Xd = torch.as_tensor(X, device="cuda")
     yd = torch.as_tensor(y, device="cuda")
     rng = np.random.default_rng(1)
@@ -191,7 +191,9 @@ def vgp_line(args, which="c3"):
     ms, n, fl, _ = _lib.prof_query("gemm_f64")
     _lib.prof_enable(False)
     desc = ("C3: 64^3 observations over [-7,7]^3, 8^3 inducing points" if which == "c3" else
-            "C5: 65,536 observations U[-2,2]^5, 4^5 inducing points, fp64")
+            "C5: 65,536 observations U[-2,2]^5, 4^5 inducing points, " +
+            ("fp64" if precision == "fp64" else
+             "M x M Cholesky in fp32 (f32 MFMA) + 3 fp64 refinement steps, the rest fp64"))
     return {"metric": "VGP ELBO Adam steps/sec", "value": 1.0 / dt, "ms_per_step": dt * 1e3,
             "config": {"workload": desc + ", EQ, optimal posterior over all N + minibatch ELBO + "
                                           "grads + Adam(0.01)", "N": N, "M": M, "d": X.shape[1],
@@ -534,6 +536,7 @@ def main():
     if world == 1 and not args.no_vgp:
         out["vgp_c3"] = vgp_line(args, "c3")
         out["vgp_c5"] = vgp_line(args, "c5")
+        out["vgp_c5_mixed"] = vgp_line(args, "c5", precision="mixed")
     if world == 1 and not args.no_c2:
         out["c2"] = c2_line()
     if world == 1 and not args.no_cpu:

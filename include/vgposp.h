@@ -145,6 +145,22 @@ int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t stride, int ba
                        double* diag_out, int* info, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Mixed-precision Cholesky (config C5, "fp32 mixed-prec Cholesky": the VGP's M x M factorizations,
+ * tf.linalg.cholesky inside tfd.VariationalGaussianProcess, main_architecture_2_sampledistribution
+ * .py:223-265): fp32 factor of A on the f32 matrix cores (v_mfma_f32_16x16x4_f32), then `iters`
+ * fp64 refinement steps X <- (I - Phi(X A X^T - I)) X of X0 = L32^-1 (Phi: lower part, diagonal
+ * halved), which converge quadratically to the fp64 inverse Cholesky factor.
+ *   A: full symmetric n x n (lda), not modified.  Linv (ldl, != A) <- L^-1, zeros above the
+ *   diagonal (what vgposp_potrf_lower(invert = 1) leaves in the lower triangle).  diag_out [n] (or
+ *   NULL) <- diag(L) = 1 / diag(L^-1).  resid (device double or NULL) <- max|X A X^T - I| of the
+ *   last step.  info: k > 0 = fp32 pivot k not positive; n + 1 = not converged (resid > 1e-6).
+ * --------------------------------------------------------------------------------------------- */
+size_t vgposp_potrf_mixed_workspace_bytes(int64_t n);
+int vgposp_potrf_mixed(const double* A, int64_t n, int64_t lda, double* Linv, int64_t ldl,
+                       double* diag_out, int iters, double* resid, int* info, void* ws,
+                       size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * The Cholesky of ONE matrix distributed over R ranks (one process per GPU) that each hold the
  * whole matrix: the O(N^3) factorization behind placement_algorithm2.py:151-219's pinv calls,
  * which the candidate-sharded placement would otherwise replicate on every rank.

@@ -62,7 +62,7 @@ def test_c2_assembly_and_potrf():
     torch.cuda.empty_cache()
 
 
-def _vgp_case(which):
+def _vgp_case(which, precision="fp64"):
     from vgposp_amd import linalg
     from vgposp_amd.vgp_training import VGPObjective
     from vgposp_amd.workloads import vgp_c3_data, vgp_c5_data
@@ -72,7 +72,7 @@ def _vgp_case(which):
     B = N // 8
     bi = np.random.default_rng(3).integers(0, N, B)
     a, l, s = _sp(0.54), 1e-5 + _sp(0.54), _sp(0.54)
-    obj = VGPObjective("eq", X, y)
+    obj = VGPObjective("eq", X, y, precision=precision)
     dev = lambda v: torch.tensor(v, dtype=torch.float64, device="cuda")  # noqa: E731
     E, ga, gl, gs, gZ = obj.loss_and_grads(linalg.as_device(Z), dev(a), dev(l), dev(s),
                                            linalg.as_device(X[bi]), linalg.as_device(y[bi]), B / N)
@@ -83,6 +83,7 @@ def _vgp_case(which):
     for g, r in zip(got[1:4], ref[1:4]):
         assert abs(g - r) <= 1e-6 * scale, (g, r)
     np.testing.assert_allclose(got[4], ref[4], rtol=0, atol=1e-6 * scale)
+    return got
 
 
 @pytest.mark.timeout(400)
@@ -93,6 +94,13 @@ def test_c3_vgp_loss_and_grads_vs_oracle():
 @pytest.mark.timeout(400)
 def test_c5_vgp_loss_and_grads_vs_oracle():
     _vgp_case("c5")
+
+
+@pytest.mark.timeout(400)
+def test_c5_vgp_mixed_precision_vs_oracle():
+    """C5 as named: the M x M factorizations in fp32 + fp64 refinement (vgposp_potrf_mixed).  ELBO
+    and gradients within the fp64 tolerances of the oracle (north_star asks 1e-5 relative)."""
+    _vgp_case("c5", precision="mixed")
 
 
 @pytest.mark.timeout(400)

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--shapes", action="store_true", help="per-shape GEMM / per-kernel dump")
     ap.add_argument("--c5", action="store_true", help="config C5: 65,536 x 5-D, M = 4^5, B = 8192")
+    ap.add_argument("--mixed", action="store_true", help="fp32 Cholesky + fp64 refinement")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     if args.c5:
@@ -41,7 +42,8 @@ def main():
     else:
         X, y, Z = vgp_c3_data(args.n, args.m)
     N, B = len(X), args.batch
-    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B)
+    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B,
+                                          precision="mixed" if args.mixed else "fp64")
     rng = np.random.default_rng(1)
     Xd = torch.as_tensor(X, device="cuda")
     yd = torch.as_tensor(y, device="cuda")
@@ -65,7 +67,8 @@ def main():
     torch.cuda.synchronize()
     dt_eager = (time.perf_counter() - t1) / args.steps
     prof = {}
-    for name in ("kernel_matrix", "gemm_f64", "gemv_f64", "kernel_vjp", "potrf_diag"):
+    for name in ("kernel_matrix", "gemm_f64", "gemv_f64", "kernel_vjp", "potrf_diag", "gemm_f32",
+                 "potrf_diag_f32"):
         ms, launches, flops, nbytes = _lib.prof_query(name)
         if launches:
             prof[name] = {"ms_per_step": ms / args.steps, "launches_per_step": launches / args.steps,

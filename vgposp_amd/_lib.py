@@ -124,6 +124,9 @@ SIGNATURES = {
                                      ctypes.POINTER(_size)]),
     "vgposp_greedy_finish_slab": (_i32, [_c_void_p, _i64, _i64, _i32, _i64, _i64, _c_void_p,
                                          _size, _c_void_p, _size, _c_void_p]),
+    "vgposp_potrf_mixed_workspace_bytes": (_size, [_i64]),
+    "vgposp_potrf_mixed": (_i32, [_c_void_p, _i64, _i64, _c_void_p, _i64, _c_void_p, _i32,
+                                  _c_void_p, _c_void_p, _c_void_p, _size, _c_void_p]),
     "vgposp_potrf_split": (_i64, [_i64]),
     "vgposp_potrf_block": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _c_void_p, _c_void_p, _size,
                                   _c_void_p]),

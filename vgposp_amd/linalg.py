@@ -160,6 +160,29 @@ def cholesky_(A, invert=False, check=True, ldiag=None):
     return A, ldiag, info
 
 
+def cholesky_inv_mixed(A, iters=3, check=True):
+    """Mixed-precision inverse Cholesky factor of a full symmetric [n, n] A (config C5): fp32 factor
+    on the f32 matrix cores, ``iters`` fp64 refinement steps (vgposp_potrf_mixed).  Returns
+    (L^-1 with zeros above the diagonal, diag(L) [n], info [1], resid [1] = max|X A X^T - I| of the
+    last step); A is not modified."""
+    A = as_device(A)
+    if A.dim() != 2 or A.shape[0] != A.shape[1]:
+        raise ValueError("A must be square")
+    if not A.is_contiguous():
+        A = A.contiguous()
+    n = A.shape[0]
+    Li = torch.empty((n, n), dtype=F64, device=A.device)
+    ldiag = torch.empty(n, dtype=F64, device=A.device)
+    info = torch.empty(1, dtype=torch.int32, device=A.device)
+    resid = torch.empty(1, dtype=F64, device=A.device)
+    ws = workspace(query("vgposp_potrf_mixed_workspace_bytes", n))
+    call("vgposp_potrf_mixed", _p(A), n, A.stride(0), _p(Li), Li.stride(0), _p(ldiag), int(iters),
+         _p(resid), _p(info), _p(ws), ws.numel(), _stream())
+    if check:
+        check_info(info)
+    return Li, ldiag, info, resid
+
+
 def cholesky(A):
     """Return the lower Cholesky factor L (zeros above the diagonal) of a copy of A."""
     L = as_device(A).clone()

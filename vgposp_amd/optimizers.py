@@ -31,16 +31,17 @@ class AdamOptimizer:
         self.epsilon = float(epsilon)
         self.name = name
 
-    def minimize(self, loss, var_list=None, group=None):
+    def minimize(self, loss, var_list=None, group=None, precision="fp64"):
         """``loss``: ``-log_prob`` of a GaussianProcess (a ``Negated`` LogProb, see ``negate``;
         gp_functions.tf_train_gp_adam) -> ``GPTrainOp``, or a VGP ``variational_loss``
         (variational_Gaussian_process_example.py:95-102) -> ``VGPTrainOp``.  ``group``: a
-        torch.distributed group over which the VGP's observations are sharded."""
+        torch.distributed group over which the VGP's observations are sharded.  ``precision``
+        (VGP only): "mixed" factors the M x M matrices in fp32 with fp64 refinement (config C5)."""
         from .distributions import VariationalLoss
         if isinstance(loss, Negated):
             return GPTrainOp(loss.log_prob, self, var_list)
         if isinstance(loss, VariationalLoss):
-            return VGPTrainOp(loss, self, var_list, group)
+            return VGPTrainOp(loss, self, var_list, group, precision=precision)
         raise TypeError("minimize() expects -log_prob (a Negated LogProb) or a VGP "
                         "variational_loss")
 
@@ -127,7 +128,7 @@ class VGPTrainOp:
     the same fixed graph a TF1 session runs.  Eager when ``graph=False``, ``VGPOSP_GRAPH=0``, for
     a data-parallel ``group``, or while the library's event timing is on."""
 
-    def __init__(self, loss, opt, var_list=None, group=None, graph=True):
+    def __init__(self, loss, opt, var_list=None, group=None, graph=True, precision="fp64"):
         from .vgp_training import VGPObjective
         vgp = loss.vgp
         spec = getattr(vgp.variational_loc, "_vgposp_posterior", None)
@@ -173,7 +174,8 @@ class VGPTrainOp:
         self.objective = VGPObjective(kernel.kind, spec["observation_index_points"],
                                       spec["observations"], jitter=vgp.jitter,
                                       posterior_jitter=spec["jitter"],
-                                      trace_adjoint=vgp.trace_adjoint, group=group)
+                                      trace_adjoint=vgp.trace_adjoint, group=group,
+                                      precision=precision)
         self.graph = bool(graph) and group is None and os.environ.get("VGPOSP_GRAPH", "1") != "0"
         self._runs = 0
         self._g = None  # (graph, feed shapes, static X, static y, loss, statuses)

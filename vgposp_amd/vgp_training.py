@@ -56,10 +56,16 @@ def kernel_vjp(kind, X1, X2, amp, ls, Kbar, u=None, w=None, want_x1bar=True):
     return grad, X1bar
 
 
-def _chol_inv(A, infos=None):
+def _chol_inv(A, infos=None, mixed=False):
     """(L^-1 with explicit zeros above the diagonal, sum log diag L) of an SPD [M, M] (copied).
     With ``infos`` (a list) the device status is appended for a later check instead of being
-    synchronised on here."""
+    synchronised on here.  mixed=True: fp32 factor + fp64 refinement (linalg.cholesky_inv_mixed,
+    config C5); the refined factor is the fp64 one to rounding."""
+    if mixed:
+        Li, ld, info, _ = linalg.cholesky_inv_mixed(A, check=infos is None)
+        if infos is not None:
+            infos.append(info)
+        return Li, torch.sum(torch.log(ld))
     Li, ld, info = linalg.cholesky_(A.clone(), invert=True, check=infos is None)
     if infos is not None:
         infos.append(info)
@@ -90,7 +96,10 @@ class VGPObjective:
     """
 
     def __init__(self, kind, X, y, jitter=1e-6, posterior_jitter=1e-6, trace_adjoint=False,
-                 group=None):
+                 group=None, precision="fp64"):
+        if precision not in ("fp64", "mixed"):
+            raise ValueError(f"precision must be 'fp64' or 'mixed', got {precision!r}")
+        self.mixed = precision == "mixed"
         self.kind = kind
         self.X = linalg.as_device(X)
         self.X = self.X[:, None] if self.X.dim() == 1 else self.X
@@ -145,9 +154,9 @@ class VGPObjective:
         M = Kzz.shape[0]
         with torch.cuda.stream(side):
             I = torch.eye(M, dtype=F64, device=Kzz.device)
-            Lzi, _ = _chol_inv(Kzz + self.j * I, infos)
-            Lpi, logdetLp = _chol_inv(Kzz + (s + 1e-6) * I, infos)
-            Lki, logdetLk = _chol_inv(Kzz, infos)
+            Lzi, _ = _chol_inv(Kzz + self.j * I, infos, self.mixed)
+            Lpi, logdetLp = _chol_inv(Kzz + (s + 1e-6) * I, infos, self.mixed)
+            Lki, logdetLk = _chol_inv(Kzz, infos, self.mixed)
             out = dict(Lzi=Lzi, Kzj_inv=_spd_inv(Lzi), Lpi=Lpi, logdetLp=logdetLp,
                        Kp_inv=_spd_inv(Lpi), Kzz_inv=_spd_inv(Lki), logdetLk=logdetLk)
         for t in out.values():
@@ -171,7 +180,7 @@ class VGPObjective:
         c = c.reshape(-1)
         Sinv = Kzz + P0 / s
         Sinv.diagonal().add_(self.pj)
-        Li, logdetL = _chol_inv(Sinv, infos)
+        Li, logdetL = _chol_inv(Sinv, infos, self.mixed)
         t = linalg.gemm(Li, linalg.gemm(Li, _col(c), tri_a=True), transa=True, tri_a=True)
         m = linalg.gemm(Kzz, t).reshape(-1) / s
         A = linalg.gemm(Li, Kzz, tri_a=True)

@@ -62,7 +62,7 @@ def c4_grid(n=128, seed=0):
     return grid_points(shape, jitter=0.05, seed=seed), shape, 2.0 * grid_spacing(shape)
 
 
-def vgp_c3_graph(X, y, Z, B, lr=0.01):
+def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64"):
     """The reference's training graph (variational_Gaussian_process_example.py:51-102) in this
     package's API -> (train_op, loss, x_batch placeholder, y_batch placeholder)."""
     from . import distributions as tfd
@@ -85,4 +85,4 @@ def vgp_c3_graph(X, y, Z, B, lr=0.01):
     yb = placeholder(np.float64, [B], name="y_train_batch")
     loss = vgp.variational_loss(observations=yb, observation_index_points=xb,
                                 kl_weight=float(B) / float(len(X)))
-    return AdamOptimizer(learning_rate=lr).minimize(loss), loss, xb, yb
+    return AdamOptimizer(learning_rate=lr).minimize(loss, precision=precision), loss, xb, yb
