@@ -6,7 +6,8 @@
 //
 // Layout: each 256-thread workgroup writes a 128-row x 128-column tile; lane pairs of columns are
 // stored as one 16-byte write per row so a wave stores 1 KiB contiguous per row.  The X2 columns
-// of the tile are held in registers, X1 rows are wave-uniform (scalar-cached) loads.
+// of the tile are held in registers; the tile's X1 rows are staged in LDS once and read back as
+// broadcasts (a global load per row put its latency in front of every row's exp and store).
 // Formula, as TFP evaluates it:  K = exp(2 log amp + log k(r / ls)).
 #include "common.h"
 #include "psd.h"
@@ -35,6 +36,7 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
                                                             double* K, int64_t ldk,
                                                             int64_t stride_k, int vec,
                                                             int tri_grid) {
+  __shared__ double xs[KM_ROWS * KM_MAXD];  // the tile's X1 rows, read back as LDS broadcasts
   const int b = blockIdx.z;
   int64_t r0, c0;
   if (tri_grid) {
@@ -46,6 +48,8 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
     c0 = (int64_t)blockIdx.x * KM_COLS;
   }
   const int dd = D > 0 ? D : d;
+  const int nrow = (int)min((int64_t)KM_ROWS, n1 - r0);
+  for (int e = threadIdx.x; e < nrow * dd; e += 256) xs[e] = X1[r0 * dd + e];
   const double a = amp[b], l = ls[b];
   const double two_log_amp = 2.0 * log(a);
   const double inv_ls = 1.0 / l;
@@ -62,14 +66,15 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
     xa[k] = (k < dd && ca < n2) ? X2[ca * dd + k] : 0.0;
     xb[k] = (k < dd && cb < n2) ? X2[cb * dd + k] : 0.0;
   }
-  const int64_t rend = min(n1, r0 + KM_ROWS);
-#pragma unroll 2
-  for (int64_t r = r0 + ty; r < rend; r += 4) {
+  __syncthreads();
+#pragma unroll 4
+  for (int i = ty; i < nrow; i += 4) {
+    const int64_t r = r0 + i;
     double da = 0.0, db = 0.0;
 #pragma unroll
     for (int k = 0; k < KM_MAXD; ++k) {
       if (k < dd) {
-        const double xr = X1[r * dd + k];
+        const double xr = xs[i * dd + k];
         const double ea = xr - xa[k], eb = xr - xb[k];
         da += ea * ea;
         db += eb * eb;

@@ -1,5 +1,7 @@
 // PSD kernel functions shared by kernel assembly, the kernel-matrix-vector product and friends.
-// As TFP evaluates them:  k(r) = exp(2 log amp + log k_unit(r / ls)).
+// TFP evaluates k(r) = exp(2 log amp + log k_unit(r / ls)); the Matern 3/2 and 5/2 forms here take
+// the polynomial factor out of the exponential (amp^2 p(s) exp(-s), no log1p: the same value to
+// rounding, and the fp64 log1p was what made Matern assembly ALU-bound).
 #pragma once
 
 #include "common.h"
@@ -15,10 +17,10 @@ __device__ __forceinline__ double kfun(double d2, double two_log_amp, double inv
   if (KIND == VGPOSP_KERNEL_MATERN12) return exp(two_log_amp - r);
   if (KIND == VGPOSP_KERNEL_MATERN32) {
     const double s = 1.7320508075688772 * r;
-    return exp(two_log_amp + log1p(s) - s);
+    return (1.0 + s) * exp(two_log_amp - s);
   }
   const double s = 2.23606797749979 * r;  // MATERN52
-  return exp(two_log_amp + log1p(s + s * s * (1.0 / 3.0)) - s);
+  return (1.0 + s + s * s * (1.0 / 3.0)) * exp(two_log_amp - s);
 }
 
 }  // namespace vgposp
