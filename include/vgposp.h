@@ -68,6 +68,17 @@ int vgposp_kernel_matrix(int kind, const double* X1, int64_t n1, const double* X
                          int batch, int uplo, double* K, int64_t ldk, int64_t stride_k,
                          void* stream);
 
+/* Kernel assembly fused with its product by a vector (the VGP's optimal posterior,
+ * variational_Gaussian_process_example.py:68-74, needs Kzx and c = Kzx y over all N observations):
+ * writes the full K (batch 1, no diagonal shift) and out[n1] = K v[n2] without re-reading K.
+ * Deterministic (per-tile partials in ws, summed in a fixed order); ws is
+ * vgposp_kernel_matrix_matvec_workspace_bytes(n1, n2) bytes. */
+size_t vgposp_kernel_matrix_matvec_workspace_bytes(int64_t n1, int64_t n2);
+int vgposp_kernel_matrix_matvec(int kind, const double* X1, int64_t n1, const double* X2,
+                                int64_t n2, int d, const double* amp, const double* ls, double* K,
+                                int64_t ldk, const double* v, double* out, void* ws,
+                                size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * fp64 GEMM on MFMA (v_mfma_f64_16x16x4f64):  C = alpha * op(A) * op(B) + beta * C
  * op(A) = A (m x k, transa=0) or A^T (A stored k x m, transa=1);
@@ -91,6 +102,57 @@ int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, int64_t k, 
                        const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                        double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int splits,
                        void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * VGP training-step glue (vgposp_amd/vgp_training.py): the non-GEMM element-wise and reduction
+ * parts of variational_loss and of the gradient TF autodiff takes through it
+ * (variational_Gaussian_process_example.py:51-102, AdamOptimizer.minimize).  Row-major fp64; s
+ * (the observation noise variance) and amp are device scalars, so the step has no host sync.
+ *   vgposp_vgp_sinv:       P0 (lower, from the SYRK) -> symmetric in place;
+ *                          Sinv = Kzz + P0 / s + pj I  (n x n, ld n)
+ *   vgposp_sym_from_lower: A's strict upper triangle <- its lower triangle
+ *   vgposp_lincomb:        out = sum_k coef[k] (s + shift)^spow[k] X[k], on i == j times
+ *                          diag_scale plus diag_coef (s + shift)^diag_spow; k <= 4, all
+ *                          rows x cols with ld
+ *   vgposp_vgp_kzz_bar:    KzzS = Kbar + Kbar^T of Kzz and G = (2 / s) Sinv_bar, from
+ *                          vecs = {u, v, qv, m_bar, t, c_bar} and mats = {HHt, P HHt, Kp^-1,
+ *                          QA QA^T, Kzz^-1, Li^T Li, Sc, Li^T A_bar} (n x n, ld n)
+ *   vgposp_dots:           out[p] = sum_i x_p[i incx_p] y_p[i incy_p] (y_p NULL: sum x) for
+ *                          op 0, sum_i log x_p[i incx_p] for op 1; p < 16, deterministic
+ *   vgposp_vgp_scalars:    out = (-E, -dE/damp, -dE/dls, -dE/dnoise) from the sums below, the
+ *                          three kernel-VJP gradients g1 (Kzz, halved inside), g2 (Kzx), g3 (Kzb)
+ * --------------------------------------------------------------------------------------------- */
+enum {
+  VGPOSP_S_RR = 0,       /* r . r, r = y_b - Kzb^T Kzj^-1 m            */
+  VGPOSP_S_KZB_H = 1,    /* <Kzb, H>, H = Kzj^-1 Kzb                   */
+  VGPOSP_S_Q_HHT = 2,    /* <Q, H H^T>                                 */
+  VGPOSP_S_PA2 = 3,      /* <Lp^-1 A, Lp^-1 A>                         */
+  VGPOSP_S_QM2 = 4,      /* |Lp^-1 m|^2                                */
+  VGPOSP_S_LOGDET_S = 5, /* sum log diag chol(Sinv)                    */
+  VGPOSP_S_LOGDET_P = 6, /* sum log diag chol(Kzz + (s + 1e-6) I)      */
+  VGPOSP_S_LOGDET_K = 7, /* sum log diag chol(Kzz)                     */
+  VGPOSP_S_TR_KPINV = 8, /* tr Kp^-1                                   */
+  VGPOSP_S_QV2 = 9,      /* |Kp^-1 m|^2                                */
+  VGPOSP_S_TR_QAQA = 10, /* tr (Kp^-1 A)(Kp^-1 A)^T                    */
+  VGPOSP_S_MB_M = 11,    /* m_bar . m                                  */
+  VGPOSP_S_G_P0 = 12,    /* <G, P0>                                    */
+  VGPOSP_S_COUNT = 13
+};
+int vgposp_vgp_sinv(double* P0, int64_t n, int64_t ldp, const double* Kzz, const double* s,
+                    double pj, double* Sinv, void* stream);
+int vgposp_sym_from_lower(double* A, int64_t n, int64_t lda, void* stream);
+int vgposp_lincomb(int64_t rows, int64_t cols, int64_t ld, int nterms, const double* const* X,
+                   const double* coef, const int* spow, double diag_scale, double diag_coef,
+                   int diag_spow, const double* s, double shift, double* out, void* stream);
+int vgposp_vgp_kzz_bar(int64_t n, const double* const* vecs, const double* const* mats,
+                       const double* s, double w, double* KzzS, double* G, void* stream);
+size_t vgposp_dots_workspace_bytes(int ndots);
+int vgposp_dots(int ndots, const double* const* x, const int64_t* incx, const double* const* y,
+                const int64_t* incy, const int64_t* len, const int* op, double* out, void* ws,
+                size_t ws_bytes, void* stream);
+int vgposp_vgp_scalars(const double* sums, const double* s, const double* amp, const double* g1,
+                       const double* g2, const double* g3, double nb, double m, double w,
+                       double jitter, double* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Vector-Jacobian product of kernel assembly: the reverse pass TF autodiff runs through

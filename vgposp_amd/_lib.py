@@ -65,6 +65,22 @@ SIGNATURES = {
     "vgposp_gemm_splitk": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p,
                                   _i64, _f64, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p,
                                   _size, _c_void_p]),
+    "vgposp_kernel_matrix_matvec_workspace_bytes": (_size, [_i64, _i64]),
+    "vgposp_kernel_matrix_matvec": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32,
+                                           _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                           _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_vgp_sinv": (_i32, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _f64, _c_void_p,
+                               _c_void_p]),
+    "vgposp_sym_from_lower": (_i32, [_c_void_p, _i64, _i64, _c_void_p]),
+    "vgposp_lincomb": (_i32, [_i64, _i64, _i64, _i32, _c_void_p, _c_void_p, _c_void_p, _f64, _f64,
+                              _i32, _c_void_p, _f64, _c_void_p, _c_void_p]),
+    "vgposp_vgp_kzz_bar": (_i32, [_i64, _c_void_p, _c_void_p, _c_void_p, _f64, _c_void_p,
+                                  _c_void_p, _c_void_p]),
+    "vgposp_dots_workspace_bytes": (_size, [_i32]),
+    "vgposp_dots": (_i32, [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                           _c_void_p, _c_void_p, _size, _c_void_p]),
+    "vgposp_vgp_scalars": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                  _c_void_p, _f64, _f64, _f64, _f64, _c_void_p, _c_void_p]),
     "vgposp_kernel_vjp_workspace_bytes": (_size, [_i64, _i64, _i32]),
     "vgposp_kernel_vjp": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p,
                                  _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p,

@@ -12,6 +12,9 @@
 #include "common.h"
 #include "psd.h"
 
+// the MV variant keeps a cross-lane sum inside the unrolled row loop, which blocks the unroll there
+#pragma clang diagnostic ignored "-Wpass-failed"
+
 namespace vgposp {
 
 constexpr int KM_ROWS = 128;
@@ -28,14 +31,18 @@ __device__ __forceinline__ int km_tri_root(int64_t id) {
 // One 128 x 128 tile per workgroup; a lower-triangular launch enumerates only the tiles on or
 // below the diagonal (blockIdx.x = ti (ti + 1) / 2 + tj).  Stores are non-temporal: K is far
 // larger than the caches and is next read by the factorization.
-template <int KIND, int D>
+// MV (full, batch 1): also the tile's share of K v — part[row][column tile] = sum over the tile's
+// columns of K[row][col] v[col], one wave sum per row (kernel_matvec_reduce_kernel adds the
+// column tiles in a fixed order), so K is never re-read for the product.
+template <int KIND, int D, bool MV>
 __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, int64_t n1,
                                                             const double* X2, int64_t n2, int d,
                                                             const double* amp, const double* ls,
                                                             const double* diag_shift, int uplo,
                                                             double* K, int64_t ldk,
                                                             int64_t stride_k, int vec,
-                                                            int tri_grid) {
+                                                            int tri_grid, const double* v = nullptr,
+                                                            double* part = nullptr) {
   __shared__ double xs[KM_ROWS * KM_MAXD];  // the tile's X1 rows, read back as LDS broadcasts
   const int b = blockIdx.z;
   int64_t r0, c0;
@@ -66,6 +73,7 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
     xa[k] = (k < dd && ca < n2) ? X2[ca * dd + k] : 0.0;
     xb[k] = (k < dd && cb < n2) ? X2[cb * dd + k] : 0.0;
   }
+  const double wa = (MV && ca < n2) ? v[ca] : 0.0, wb = (MV && cb < n2) ? v[cb] : 0.0;
   __syncthreads();
 #pragma unroll 4
   for (int i = ty; i < nrow; i += 4) {
@@ -96,19 +104,38 @@ __global__ __launch_bounds__(256) void kernel_matrix_kernel(const double* X1, in
       if (oka) __builtin_nontemporal_store(va, row + ca);
       if (okb) __builtin_nontemporal_store(vb, row + cb);
     }
+    if (MV) {
+      const double sum = wave_sum(va * wa + vb * wb);
+      if (tx == 0) part[r * gridDim.x + blockIdx.x] = sum;
+    }
   }
 }
 
-template <int KIND>
+// out[r] = sum over the column tiles of part[r][tile]: one workgroup per row, a fixed summation
+// order (deterministic).
+__global__ __launch_bounds__(256) void kernel_matvec_reduce_kernel(int64_t ntiles,
+                                                                   const double* part, double* out) {
+  __shared__ double red[4];
+  const int64_t r = blockIdx.x;
+  const double* row = part + r * ntiles;
+  double s = 0.0;
+  for (int64_t t = threadIdx.x; t < ntiles; t += 256) s += row[t];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[r] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+template <int KIND, bool MV = false>
 static void launch_kind(dim3 g, hipStream_t s, const double* X1, int64_t n1, const double* X2,
                         int64_t n2, int d, const double* amp, const double* ls,
                         const double* shift, int uplo, double* K, int64_t ldk, int64_t stride,
-                        int vec, int tri_grid) {
+                        int vec, int tri_grid, const double* v = nullptr, double* part = nullptr) {
   switch (d) {
-    case 1: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 1>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
-    case 2: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 2>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
-    case 3: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 3>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
-    default: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 0>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid); break;
+    case 1: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 1, MV>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid, v, part); break;
+    case 2: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 2, MV>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid, v, part); break;
+    case 3: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 3, MV>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid, v, part); break;
+    default: hipLaunchKernelGGL((kernel_matrix_kernel<KIND, 0, MV>), g, dim3(256), 0, s, X1, n1, X2, n2, d, amp, ls, shift, uplo, K, ldk, stride, vec, tri_grid, v, part); break;
   }
 }
 
@@ -152,6 +179,56 @@ extern "C" int vgposp_kernel_matrix(int kind, const double* X1, int64_t n1, cons
     case VGPOSP_KERNEL_MATERN32: launch_kind<VGPOSP_KERNEL_MATERN32>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec, tri_grid); break;
     default: launch_kind<VGPOSP_KERNEL_MATERN52>(g, s, X1, n1, X2, n2, d, amp, ls, diag_shift, uplo, K, ldk, stride_k, vec, tri_grid); break;
   }
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" size_t vgposp_kernel_matrix_matvec_workspace_bytes(int64_t n1, int64_t n2) {
+  if (n1 <= 0 || n2 <= 0) return 0;
+  return 8 * (size_t)(ceil_div(n2, KM_COLS) * n1);
+}
+
+extern "C" int vgposp_kernel_matrix_matvec(int kind, const double* X1, int64_t n1,
+                                           const double* X2, int64_t n2, int d, const double* amp,
+                                           const double* ls, double* K, int64_t ldk,
+                                           const double* v, double* out, void* ws, size_t ws_bytes,
+                                           void* stream) {
+  clear_error();
+  VG_CHECK_ARG(kind >= VGPOSP_KERNEL_EQ && kind <= VGPOSP_KERNEL_MATERN52, 1);
+  VG_CHECK_ARG(X1 != nullptr, 2);
+  VG_CHECK_ARG(n1 >= 1, 3);
+  VG_CHECK_ARG(X2 != nullptr, 4);
+  VG_CHECK_ARG(n2 >= 1, 5);
+  VG_CHECK_ARG(d >= 1 && d <= KM_MAXD, 6);
+  VG_CHECK_ARG(amp != nullptr, 7);
+  VG_CHECK_ARG(ls != nullptr, 8);
+  VG_CHECK_ARG(K != nullptr, 9);
+  VG_CHECK_ARG(ldk >= n2, 10);
+  VG_CHECK_ARG(v != nullptr, 11);
+  VG_CHECK_ARG(out != nullptr, 12);
+  VG_CHECK_ARG(ws != nullptr, 13);
+  const int64_t ntiles = ceil_div(n2, KM_COLS);
+  if (ws_bytes < 8 * (size_t)(ntiles * n1)) {
+    set_error("vgposp_kernel_matrix_matvec: workspace %zu < %zu bytes", ws_bytes,
+              8 * (size_t)(ntiles * n1));
+    return VGPOSP_E_WS;
+  }
+  double* part = static_cast<double*>(ws);
+  const dim3 g((unsigned)ntiles, (unsigned)ceil_div(n1, KM_ROWS), 1u);
+  const int vec = (reinterpret_cast<uintptr_t>(K) % 16 == 0) && (ldk % 2 == 0);
+  hipStream_t s = as_stream(stream);
+  {
+    ProfScope ps("kernel_matrix", s, 0.0, 8.0 * ((double)n1 * n2 + (double)d * (n1 + n2) + n2));
+    switch (kind) {
+      case VGPOSP_KERNEL_EQ: launch_kind<VGPOSP_KERNEL_EQ, true>(g, s, X1, n1, X2, n2, d, amp, ls, nullptr, VGPOSP_FULL, K, ldk, 0, vec, 0, v, part); break;
+      case VGPOSP_KERNEL_MATERN12: launch_kind<VGPOSP_KERNEL_MATERN12, true>(g, s, X1, n1, X2, n2, d, amp, ls, nullptr, VGPOSP_FULL, K, ldk, 0, vec, 0, v, part); break;
+      case VGPOSP_KERNEL_MATERN32: launch_kind<VGPOSP_KERNEL_MATERN32, true>(g, s, X1, n1, X2, n2, d, amp, ls, nullptr, VGPOSP_FULL, K, ldk, 0, vec, 0, v, part); break;
+      default: launch_kind<VGPOSP_KERNEL_MATERN52, true>(g, s, X1, n1, X2, n2, d, amp, ls, nullptr, VGPOSP_FULL, K, ldk, 0, vec, 0, v, part); break;
+    }
+    VG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(kernel_matvec_reduce_kernel, dim3((unsigned)n1), dim3(256), 0, s, ntiles, part,
+                     out);
   VG_LAUNCH_CHECK();
   return 0;
 }

@@ -97,6 +97,22 @@ def kernel_matrix(kind, X1, X2=None, amp=1.0, ls=1.0, diag_shift=None, lower=Fal
     return out
 
 
+def kernel_matrix_matvec(kind, X1, X2, amp, ls, v, out_K, out_v):
+    """out_K [n1, n2] <- K(X1, X2) (one amplitude / length scale) and out_v [n1] <- K v in one
+    pass (vgposp_kernel_matrix_matvec: K is never re-read for the product)."""
+    X1, X2, v = as_device(X1), as_device(X2), as_device(v).reshape(-1)
+    X1 = X1[:, None] if X1.dim() == 1 else X1
+    X2 = X2[:, None] if X2.dim() == 1 else X2
+    n1, n2, d = X1.shape[0], X2.shape[0], X1.shape[1]
+    if out_K.shape[-2:] != (n1, n2) or v.numel() != n2 or out_v.numel() != n1:
+        raise ValueError("kernel_matrix_matvec: shapes do not match")
+    a, l = _vec(amp, 1), _vec(ls, 1)
+    ws = workspace(query("vgposp_kernel_matrix_matvec_workspace_bytes", n1, n2))
+    call("vgposp_kernel_matrix_matvec", kind_id(kind), _p(X1), n1, _p(X2), n2, d, _p(a), _p(l),
+         _p(out_K), out_K.stride(-2), _p(v), _p(out_v), _p(ws), ws.numel(), _stream())
+    return out_K, out_v
+
+
 def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=False,
          tri_a=False, tri_b=False, splitk=True):
     """C = alpha op(A) op(B) + beta C on fp64 MFMA (2-D operands).  ``splitk=True`` lets the

@@ -28,16 +28,13 @@ replicated and never reduced.
 """
 from __future__ import annotations
 
-import math
+import ctypes
 
 import torch
 
 from . import linalg
 from ._lib import call, query
 from .linalg import F64, _p, _stream, kind_id
-
-LOG_2PI = math.log(2.0 * math.pi)
-
 
 def kernel_vjp(kind, X1, X2, amp, ls, Kbar, u=None, w=None, want_x1bar=True):
     """(grad[2] = (d/damp, d/dls), X1bar [n1, d] or None) of sum(Kbar * K(X1, X2))
@@ -56,29 +53,58 @@ def kernel_vjp(kind, X1, X2, amp, ls, Kbar, u=None, w=None, want_x1bar=True):
     return grad, X1bar
 
 
-def _chol_inv(A, infos=None, mixed=False):
-    """(L^-1 with explicit zeros above the diagonal, sum log diag L) of an SPD [M, M] (copied).
-    With ``infos`` (a list) the device status is appended for a later check instead of being
-    synchronised on here.  mixed=True: fp32 factor + fp64 refinement (linalg.cholesky_inv_mixed,
-    config C5); the refined factor is the fp64 one to rounding."""
+def _chol_inv(A, infos=None, mixed=False, inplace=False):
+    """(L^-1 in the lower triangle, diag L [M]) of an SPD [M, M].  The upper triangle of the
+    result is NOT zeroed: every consumer reads it as a stored-lower-triangular GEMM operand
+    (tri_a / tri_b).  ``inplace`` factors A itself instead of a copy.  With ``infos`` (a list) the
+    device status is appended for a later check instead of being synchronised on here.
+    mixed=True: fp32 factor + fp64 refinement (linalg.cholesky_inv_mixed, config C5); the refined
+    factor is the fp64 one to rounding."""
     if mixed:
         Li, ld, info, _ = linalg.cholesky_inv_mixed(A, check=infos is None)
-        if infos is not None:
-            infos.append(info)
-        return Li, torch.sum(torch.log(ld))
-    Li, ld, info = linalg.cholesky_(A.clone(), invert=True, check=infos is None)
+    else:
+        Li, ld, info = linalg.cholesky_(A if inplace else A.clone(), invert=True,
+                                        check=infos is None)
+        ld = ld.reshape(-1)
     if infos is not None:
         infos.append(info)
-    return torch.tril(Li), torch.sum(torch.log(ld))
+    return Li, ld
+
+
+def _ptrs(ts):
+    return (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+def _lincomb(terms, s=None, shift=0.0, diag_scale=1.0, diag=(0.0, 0), out=None):
+    """out = sum c (s + shift)^e X over terms [(X, c, e)] (same shape, contiguous), on the
+    diagonal of a square out times diag_scale plus diag[0] (s + shift)^diag[1]
+    (vgposp_lincomb: one launch, s read on device)."""
+    X0 = terms[0][0]
+    if out is None:
+        out = torch.empty_like(X0)
+    rows, cols = (X0.shape[0], X0.shape[1]) if X0.dim() == 2 else (1, X0.numel())
+    xs = _ptrs([t[0] for t in terms])
+    cs = (ctypes.c_double * len(terms))(*[float(t[1]) for t in terms])
+    es = (ctypes.c_int * len(terms))(*[int(t[2]) for t in terms])
+    call("vgposp_lincomb", rows, cols, cols, len(terms), xs, cs, es, float(diag_scale),
+         float(diag[0]), int(diag[1]), _p(s), float(shift), _p(out), _stream())
+    return out
+
+
+def _dots(pairs, out):
+    """out[p] = the p-th of [(x, incx, y or None, incy, n, op)] (vgposp_dots, op 1 = sum log)."""
+    n = len(pairs)
+    ws = linalg.workspace(query("vgposp_dots_workspace_bytes", n))
+    call("vgposp_dots", n, _ptrs([q[0] for q in pairs]),
+         (ctypes.c_int64 * n)(*[q[1] for q in pairs]), _ptrs([q[2] for q in pairs]),
+         (ctypes.c_int64 * n)(*[q[3] for q in pairs]), (ctypes.c_int64 * n)(*[q[4] for q in pairs]),
+         (ctypes.c_int * n)(*[q[5] for q in pairs]), _p(out), _p(ws), ws.numel(), _stream())
+    return out
 
 
 def _spd_inv(Li):
     """A^-1 = L^-T L^-1 (full) from L^-1."""
     return linalg.gemm(Li, Li, transa=True, tri_a=True, tri_b=True)
-
-
-def _sym_from_lower(P):
-    return torch.tril(P) + torch.tril(P, -1).t()
 
 
 def _col(v):
@@ -126,11 +152,13 @@ class VGPObjective:
             dist.all_reduce(t, group=self.group)
         return t
 
-    def _kzx(self, Z, a, l):
+    def _kzx(self, Z, a, l, c):
+        """Kzx = K(Z, X) [M, N] and c <- Kzx y in one pass over Kzx."""
         M, N = Z.shape[0], self.X.shape[0]
         if self._Kzx is None or self._Kzx.shape != (M, N):
-            self._Kzx = torch.empty((1, M, N), dtype=F64, device=self.X.device)
-        return linalg.kernel_matrix(self.kind, Z, self.X, a, l, out=self._Kzx)[0]
+            self._Kzx = torch.empty((M, N), dtype=F64, device=self.X.device)
+        linalg.kernel_matrix_matvec(self.kind, Z, self.X, a, l, self.y, self._Kzx, c)
+        return self._Kzx
 
     def optimal_posterior(self, Z, amp, ls, noise):
         """(loc [M], scale [M, M]) of optimal_variational_posterior over all shards."""
@@ -140,53 +168,65 @@ class VGPObjective:
         st = self._forward_posterior(Z, a, l, s)
         return st["m"], st["A"]
 
-    def _kzz_factors(self, Kzz, s, infos):
+    def _kzz_factors(self, Kzz, s, infos, fork):
         """The three Cholesky + inverse factorizations that need only Kzz (Kzz + jitter I for the
-        VGP, Kzz + (noise + 1e-6) I for the KL prior, Kzz itself for log|det A|), enqueued on a
-        side stream so that their latency-bound leaves overlap the Kzx assembly and the split-K
-        Kzx Kzx^T on the main stream.  The caller waits on the returned stream before use."""
+        VGP, Kzz + (noise + 1e-6) I for the KL prior, Kzz itself for log|det A|), each on its own
+        side stream, so that their latency-bound leaves run beside one another and beside the
+        Kzx assembly and the split-K Kzx Kzx^T already enqueued on the main stream.  ``fork`` is
+        the main-stream event recorded right after Kzz: the side chains depend on nothing later.
+        (Captured into the step's HIP graph, the heavy main-stream nodes come first in capture
+        order, so they are dispatched first.)  The caller waits on the returned streams."""
         main = torch.cuda.current_stream()
         if self._side is None:
-            self._side = torch.cuda.Stream()
-        side = self._side
-        side.wait_stream(main)
-        Kzz.record_stream(side)
-        M = Kzz.shape[0]
-        with torch.cuda.stream(side):
-            I = torch.eye(M, dtype=F64, device=Kzz.device)
-            Lzi, _ = _chol_inv(Kzz + self.j * I, infos, self.mixed)
-            Lpi, logdetLp = _chol_inv(Kzz + (s + 1e-6) * I, infos, self.mixed)
-            Lki, logdetLk = _chol_inv(Kzz, infos, self.mixed)
-            out = dict(Lzi=Lzi, Kzj_inv=_spd_inv(Lzi), Lpi=Lpi, logdetLp=logdetLp,
-                       Kp_inv=_spd_inv(Lpi), Kzz_inv=_spd_inv(Lki), logdetLk=logdetLk)
-        for t in out.values():
+            self._side = [torch.cuda.Stream() for _ in range(3)]
+        res = []
+        for i, st in enumerate(self._side):
+            st.wait_event(fork)
+            Kzz.record_stream(st)
+            s.record_stream(st)
+            with torch.cuda.stream(st):
+                A = Kzz.clone()
+                if i == 0:
+                    A.diagonal().add_(self.j)
+                elif i == 1:  # computed on this stream: it depends only on s (before the fork)
+                    A.diagonal().add_(s + 1e-6)
+                mine = []
+                Li, ld = _chol_inv(A, mine, self.mixed, inplace=True)
+                res.append((Li, ld, _spd_inv(Li), mine))
+        (Lzi, _, Kzj_inv, i1), (Lpi, ldp, Kp_inv, i2), (Lki, ldk, Kzz_inv, i3) = res
+        infos.extend(i1 + i2 + i3)
+        out = dict(Lzi=Lzi, Kzj_inv=Kzj_inv, Lpi=Lpi, ldp=ldp, Kp_inv=Kp_inv, Kzz_inv=Kzz_inv,
+                   ldk=ldk)
+        for t in list(out.values()) + infos:
             t.record_stream(main)
-        for t in infos:
-            t.record_stream(main)
-        return out, side
+        return out, self._side
 
     def _forward_posterior(self, Z, a, l, s, infos=None, side=False):
         M = Z.shape[0]
         Kzz = linalg.kernel_matrix(self.kind, Z, Z, a, l)[0]
-        fac = self._kzz_factors(Kzz, s, infos) if side else None
-        Kzx = self._kzx(Z, a, l)
+        fork = None
+        if side:
+            fork = torch.cuda.Event()
+            fork.record()
         red = torch.empty(M * M + M, dtype=F64, device=Z.device)
         P0 = red[:M * M].view(M, M)
         c = red[M * M:].view(M, 1)
+        Kzx = self._kzx(Z, a, l, c)  # c = Kzx y fused into the assembly
         linalg.gemm(Kzx, Kzx, P0, transb=True, lower_c=True, splitk=True)
-        linalg.gemm(Kzx, _col(self.y), c)
+        fac = self._kzz_factors(Kzz, s, infos, fork) if side else None
         self._allreduce(red)
-        P0 = _sym_from_lower(P0)
+        # P0 -> symmetric in place, Sinv = Kzz + P0 / s + pj I (one launch)
+        Sinv = torch.empty((M, M), dtype=F64, device=Z.device)
+        call("vgposp_vgp_sinv", _p(P0), M, M, _p(Kzz), _p(s), self.pj, _p(Sinv), _stream())
         c = c.reshape(-1)
-        Sinv = Kzz + P0 / s
-        Sinv.diagonal().add_(self.pj)
-        Li, logdetL = _chol_inv(Sinv, infos, self.mixed)
+        Li, lds = _chol_inv(Sinv, infos, self.mixed, inplace=True)
         t = linalg.gemm(Li, linalg.gemm(Li, _col(c), tri_a=True), transa=True, tri_a=True)
         m = linalg.gemm(Kzz, t).reshape(-1) / s
         A = linalg.gemm(Li, Kzz, tri_a=True)
-        st = dict(Kzz=Kzz, Kzx=Kzx, P0=P0, c=c, Li=Li, logdetL=logdetL, t=t.reshape(-1), m=m, A=A)
+        st = dict(Kzz=Kzz, Kzx=Kzx, P0=P0, c=c, Li=Li, lds=lds, t=t.reshape(-1), m=m, A=A)
         if fac is not None:
-            torch.cuda.current_stream().wait_stream(fac[1])
+            for stream in fac[1]:
+                torch.cuda.current_stream().wait_stream(stream)
             st.update(fac[0])
         return st
 
@@ -205,98 +245,90 @@ class VGPObjective:
         M, nb = Z.shape[0], yb.numel()
         check = infos is None
         infos = [] if check else infos  # Cholesky statuses, checked once at the end
-        # every 1 / s factor is applied on device to an M x M operand (no host copy of s)
-        s_inv = 1.0 / s
         st = self._forward_posterior(Z, a, l, s, infos, side=True)
-        Kzz, Kzx, P0, c, Li, logdetL, t, m, A = (st[k] for k in
-                                                 ("Kzz", "Kzx", "P0", "c", "Li", "logdetL", "t",
-                                                  "m", "A"))
+        Kzz, Kzx, P0, c, Li, t, m, A = (st[k] for k in
+                                        ("Kzz", "Kzx", "P0", "c", "Li", "t", "m", "A"))
         Kzb = linalg.kernel_matrix(self.kind, Z, Xb, a, l)[0]
-        # ---- variational loss ----
-        Lzi, Kzj_inv, Lpi, logdetLp, Kp_inv, Kzz_inv, logdetLk = (
-            st[k] for k in ("Lzi", "Kzj_inv", "Lpi", "logdetLp", "Kp_inv", "Kzz_inv", "logdetLk"))
+        Kzj_inv, Lpi, Kp_inv, Kzz_inv = (st[k] for k in ("Kzj_inv", "Lpi", "Kp_inv", "Kzz_inv"))
+        dev = Z.device
+        # ---- variational loss (every scalar is taken at the end by vgposp_dots / _scalars) ----
         v = linalg.gemm(Kzj_inv, _col(m))
-        r = yb - linalg.gemm(Kzb, v, transa=True).reshape(-1)
+        r = yb.clone()
+        linalg.gemm(Kzb, v, _col(r), alpha=-1.0, beta=1.0, transa=True)  # r = yb - Kzb^T v
         v = v.reshape(-1)
-        s2 = s + j
-        rr = torch.dot(r, r)
-        obs = -0.5 * rr / s2 - 0.5 * nb * torch.log(2.0 * math.pi * s2)
         # Trace term with two M x B products instead of three: with H = Kzj^-1 Kzb (Kzj^-1 =
         # Lzi^T Lzi) and R = op(A) H,  tr(G^T G) = <Kzb, H> for G = Lzi Kzb, and
         # tr(R^T R) = <Q, H H^T> with Q = A^T A (A A^T for the trace_adjoint form).
         H = linalg.gemm(Kzj_inv, Kzb)
-        HHt = _sym_from_lower(linalg.gemm(H, H, transb=True, lower_c=True))
+        HHt = linalg.gemm(H, H, transb=True, lower_c=True)
+        call("vgposp_sym_from_lower", _p(HHt), M, M, _stream())
         Q = linalg.gemm(A, A, transa=not self.trace_adjoint, transb=self.trace_adjoint)
-        T = 0.5 * (nb * a * a - torch.dot(Kzb.reshape(-1), H.reshape(-1)) + torch.sum(Q * HHt)) / s
-        logdetA = 2.0 * logdetLk - logdetL
         PA = linalg.gemm(Lpi, A, tri_a=True)
         qm = linalg.gemm(Lpi, _col(m), tri_a=True)
-        KL = logdetLp - logdetA + 0.5 * (-M + torch.sum(PA * PA) + torch.sum(qm * qm))
-        E = obs - T - w * KL
+        sums = torch.zeros(13, dtype=F64, device=dev)  # VGPOSP_S_* of vgposp.h
+        fwd = [(r, 1, r, 1, nb, 0), (Kzb, 1, H, 1, M * nb, 0), (Q, 1, HHt, 1, M * M, 0),
+               (PA, 1, PA, 1, M * M, 0), (qm, 1, qm, 1, M, 0), (st["lds"], 1, None, 0, M, 1),
+               (st["ldp"], 1, None, 0, M, 1), (st["ldk"], 1, None, 0, M, 1)]
         if not want_grads:
+            _dots(fwd, sums)
+            zero = torch.zeros(2, dtype=F64, device=dev)
+            out = torch.empty(4, dtype=F64, device=dev)
+            call("vgposp_vgp_scalars", _p(sums), _p(s), _p(a), _p(zero), _p(zero), _p(zero),
+                 float(nb), float(M), w, j, _p(out), _stream())
             if check:
                 for info in infos:
                     linalg.check_info(info)
-            return -E, None, None, None, None
+            return out[0], None, None, None, None
         # ---- reverse pass (d E) ----
-        mu_b = r / s2
-        s_b = 0.5 * rr / (s2 * s2) - 0.5 * nb / s2
+        mu_b = _lincomb([(r, 1.0, -1)], s, shift=j)  # r / (s + j)
         u = linalg.gemm(Kzj_inv, linalg.gemm(Kzb, _col(mu_b))).reshape(-1)
-        m_b = u.clone()
-        Kzz_b = -torch.outer(u, v)
-        s_b = s_b + T / s
-        a_b = -nb * a / s
-        Kzz_b -= (0.5 * s_inv) * HHt
-        # dE/dR = -R / s gives A_b = -(1/s) R H^T = -(1/s) A HHt (HHt A for trace_adjoint) and
-        # H_b = -(1/s) Q H; through H = Kzj^-1 Kzb: Kzb_b += Kzj^-1 H_b, Kzz_b -= Kzj^-1 H_b H^T.
-        # With P = Kzj^-1 Q all of it is M x M work plus one M x B product:
+        # dE/dR = -R / s gives A_b = -(1/s) A HHt (HHt A for trace_adjoint) and H_b = -(1/s) Q H;
+        # through H = Kzj^-1 Kzb: Kzb_b += Kzj^-1 H_b, Kzz_b -= Kzj^-1 H_b H^T.  With
+        # P = Kzj^-1 Q all of it is M x M work plus one M x B product:
         #   Kzb_b = H / s + Kzj^-1 H_b = ((I - P) / s) H,   Kzz_b += (1/s) P HHt.
-        A_b = (linalg.gemm(HHt, A) if self.trace_adjoint else linalg.gemm(A, HHt)) * (-s_inv)
-        P = linalg.gemm(Kzj_inv, Q)
-        Kzz_b += s_inv * linalg.gemm(P, HHt)
-        W = -P
-        W.diagonal().add_(1.0)
-        Kzb_b = linalg.gemm(W * s_inv, H)
+        AH = linalg.gemm(HHt, A) if self.trace_adjoint else linalg.gemm(A, HHt)
         QA = linalg.gemm(Kp_inv, A)
+        A_b = _lincomb([(AH, -1.0, -1), (QA, -w, 0)], s)
+        P = linalg.gemm(Kzj_inv, Q)
+        PHH = linalg.gemm(P, HHt)
+        W = _lincomb([(P, -1.0, -1)], s, diag=(1.0, -1))  # (I - P) / s
+        Kzb_b = linalg.gemm(W, H)
         qv = linalg.gemm(Kp_inv, _col(m)).reshape(-1)
-        A_b -= w * QA
-        m_b -= w * qv
-        Kp_b = Kp_inv - torch.outer(qv, qv)
-        linalg.gemm(QA, QA, Kp_b, alpha=-1.0, beta=1.0, transb=True)
-        Kp_b *= -0.5 * w
-        Kzz_b += Kp_b
-        s_b = s_b + torch.trace(Kp_b)
-        Kzz_b += w * Kzz_inv
-        Sinv_b = (-0.5 * w) * _spd_inv(Li)
-        Kzz_b += torch.outer(m_b, t) / s
+        m_b = _lincomb([(u, 1.0, 0), (qv, -w, 0)])
+        QAQA = linalg.gemm(QA, QA, transb=True)
+        LiLi = _spd_inv(Li)
         t_b = linalg.gemm(Kzz, _col(m_b)) / s
-        s_b = s_b - torch.dot(m_b, m) / s
         c_b = linalg.gemm(Li, linalg.gemm(Li, t_b, tri_a=True), transa=True, tri_a=True).reshape(-1)
-        ct = torch.outer(c_b, t)
-        Sinv_b -= 0.5 * (ct + ct.t())
-        linalg.gemm(Li, A_b, Kzz_b, beta=1.0, transa=True, tri_a=True)
-        # Cholesky adjoint: L^T Lbar = -A_b A^T  ->  sym(L^-T Phi(-A_b A^T) L^-1)
-        Pm = -torch.tril(linalg.gemm(A_b, A, transb=True))
-        Pm.diagonal().mul_(0.5)
-        Sc = linalg.gemm(Li, linalg.gemm(Pm, Li, tri_b=True), transa=True, tri_a=True)
-        Sinv_b += 0.5 * (Sc + Sc.t())
-        Kzz_b += Sinv_b
-        s_b = s_b - torch.sum(Sinv_b * P0) / (s * s)
-        # Kzx_bar = (2 / s) Sinv_b Kzx + c_b y^T  (rank-1 term fused into the VJP)
-        Kzx_b = linalg.gemm(Sinv_b * (2.0 * s_inv), Kzx)
+        LiA = linalg.gemm(Li, A_b, transa=True, tri_a=True)
+        # Cholesky adjoint: L^T Lbar = -A_b A^T  ->  sym(L^-T Phi(-A_b A^T) L^-1); Phi's lower
+        # triangle (halved diagonal) is read through tri_a, its upper part is ignored
+        Pm = _lincomb([(linalg.gemm(A_b, A, transb=True), -1.0, 0)], diag_scale=0.5)
+        Sc = linalg.gemm(Li, linalg.gemm(Pm, Li, tri_a=True, tri_b=True), transa=True, tri_a=True)
+        KzzS = torch.empty((M, M), dtype=F64, device=dev)
+        G = torch.empty((M, M), dtype=F64, device=dev)
+        call("vgposp_vgp_kzz_bar", M, _ptrs([u, v, qv, m_b, st["t"], c_b]),
+             _ptrs([HHt, PHH, Kp_inv, QAQA, Kzz_inv, LiLi, Sc, LiA]), _p(s), w, _p(KzzS), _p(G),
+             _stream())
+        # Kzx_bar = G Kzx + c_b y^T, G = (2 / s) Sinv_b  (rank-1 term fused into the VJP)
+        Kzx_b = linalg.gemm(G, Kzx)
         g2, Zb2 = kernel_vjp(self.kind, Z, self.X, a, l, Kzx_b, c_b, self.y)
-        red = torch.cat([g2, Zb2.reshape(-1)])
-        self._allreduce(red)
-        g2, Zb2 = red[:2], red[2:].view_as(Z)
-        g1, Zb1 = kernel_vjp(self.kind, Z, Z, a, l, (Kzz_b + Kzz_b.t()).contiguous())
+        if self.group is not None:
+            red = torch.cat([g2, Zb2.reshape(-1)])
+            self._allreduce(red)
+            g2, Zb2 = red[:2], red[2:].view_as(Z)
+        g1, Zb1 = kernel_vjp(self.kind, Z, Z, a, l, KzzS)
         g3, Zb3 = kernel_vjp(self.kind, Z, Xb, a, l, Kzb_b, v, mu_b)
-        a_b = a_b + 0.5 * g1[0] + g2[0] + g3[0]
-        l_b = 0.5 * g1[1] + g2[1] + g3[1]
-        Z_b = Zb1 + Zb2 + Zb3
+        rev = [(Kp_inv, M + 1, None, 0, M, 0), (qv, 1, qv, 1, M, 0), (QAQA, M + 1, None, 0, M, 0),
+               (m_b, 1, m, 1, M, 0), (G, 1, P0, 1, M * M, 0)]
+        _dots(fwd + rev, sums)
+        out = torch.empty(4, dtype=F64, device=dev)
+        call("vgposp_vgp_scalars", _p(sums), _p(s), _p(a), _p(g1), _p(g2), _p(g3), float(nb),
+             float(M), w, j, _p(out), _stream())
+        Z_b = _lincomb([(Zb1, -1.0, 0), (Zb2, -1.0, 0), (Zb3, -1.0, 0)])
         if check:
             for info in infos:
                 linalg.check_info(info)
-        return -E, -a_b, -l_b, -s_b, -Z_b
+        return out[0], out[1], out[2], out[3], Z_b
 
 
 __all__ = ["VGPObjective", "kernel_vjp"]
