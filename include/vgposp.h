@@ -91,6 +91,15 @@ int vgposp_gemm(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
                 const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                 double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, void* stream);
 
+/* Batched vgposp_gemm: element b (< batch) computes C + b sC from A + b sA and B + b sB, all in
+ * one launch (e.g. the VGP's four M x M inverse factors' L^-T L^-1).  Split-K over the workspace
+ * as vgposp_gemm_splitk when ws holds vgposp_gemm_batched_workspace_bytes, else unsplit. */
+size_t vgposp_gemm_batched_workspace_bytes(int64_t m, int64_t n, int64_t k, int uplo_c, int batch);
+int vgposp_gemm_batched(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                        const double* A, int64_t lda, int64_t sA, const double* B, int64_t ldb,
+                        int64_t sB, double beta, double* C, int64_t ldc, int64_t sC, int uplo_c,
+                        int tri_a, int tri_b, int batch, void* ws, size_t ws_bytes, void* stream);
+
 /* Split-K form of vgposp_gemm for few output tiles and a long K (e.g. the VGP's
  * Kzx Kzx^T with M = 512 inducing points and K = N = 262,144 observations: 10 lower tiles).  Each
  * of `splits` K-ranges writes alpha * partial into ws ([splits][m][n]); a second kernel sums them
@@ -109,7 +118,9 @@ int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, int64_t k, 
  * (variational_Gaussian_process_example.py:51-102, AdamOptimizer.minimize).  Row-major fp64; s
  * (the observation noise variance) and amp are device scalars, so the step has no host sync.
  *   vgposp_vgp_sinv:       P0 (lower, from the SYRK) -> symmetric in place;
- *                          Sinv = Kzz + P0 / s + pj I  (n x n, ld n)
+ *                          F[0] = Sinv = Kzz + P0 / s + pj I  (n x n, ld n); nf = 4 also
+ *                          writes F[1] = Kzz + jitter I, F[2] = Kzz + (s + 1e-6) I, F[3] = Kzz
+ *                          (the step's four M x M factorizations, done as one batch)
  *   vgposp_sym_from_lower: A's strict upper triangle <- its lower triangle
  *   vgposp_lincomb:        out = sum_k coef[k] (s + shift)^spow[k] X[k], on i == j times
  *                          diag_scale plus diag_coef (s + shift)^diag_spow; k <= 4, all
@@ -139,7 +150,7 @@ enum {
   VGPOSP_S_COUNT = 13
 };
 int vgposp_vgp_sinv(double* P0, int64_t n, int64_t ldp, const double* Kzz, const double* s,
-                    double pj, double* Sinv, void* stream);
+                    double pj, double jitter, double* F, int nf, void* stream);
 int vgposp_sym_from_lower(double* A, int64_t n, int64_t lda, void* stream);
 int vgposp_lincomb(int64_t rows, int64_t cols, int64_t ld, int nterms, const double* const* X,
                    const double* coef, const int* spow, double diag_scale, double diag_coef,
@@ -202,6 +213,10 @@ int vgposp_index_taper(double* C, int64_t n, int64_t ldc, int64_t I0, int64_t I1
  * nominators).  diag_out ([batch][n], or NULL) receives diag(L) (log-det).  info: [batch] int32.
  * ws must hold vgposp_potrf_workspace_bytes(n).
  * --------------------------------------------------------------------------------------------- */
+/* Workspace for factoring a batch of n > 128 matrices in ONE recursion (every launch covers the
+ * whole batch): pass at least this many bytes to vgposp_potrf_lower with batch > 1 (a smaller
+ * workspace of vgposp_potrf_workspace_bytes(n) factors them one after another). */
+size_t vgposp_potrf_batched_workspace_bytes(int64_t n, int batch);
 size_t vgposp_potrf_workspace_bytes(int64_t n);
 int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t stride, int batch, int invert,
                        double* diag_out, int* info, void* ws, size_t ws_bytes, void* stream);

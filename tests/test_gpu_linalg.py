@@ -252,3 +252,78 @@ def test_gemm_bottom_right_block(L, tri_a, splitk):
     L.gemm(X22, W, C, alpha=-1.0, beta=0.0, tri_a=bool(tri_a), splitk=bool(splitk))
     torch.cuda.synchronize()
     np.testing.assert_allclose(C.cpu().numpy(), ref, rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("n", [200, 513, 701, 1100])
+@pytest.mark.parametrize("invert", [False, True])
+def test_cholesky_batched_one_recursion(L, n, invert):
+    """B > 1 matrices of n > 128 run as ONE recursion (vgposp_potrf_batched_workspace_bytes):
+    every factor, inverse and diagonal equals the single-matrix result; odd n takes the
+    reference GEMM kernel's batched grid, n > 512 the block-inverse path."""
+    rng = np.random.default_rng(n + invert)
+    S = np.stack([_spd(n, rng) * (1.0 + 0.5 * b) for b in range(3)])
+    A = L.as_device(S.copy())
+    A, ld, info = L.cholesky_(A, invert=invert)
+    assert int(info.abs().sum()) == 0
+    il = np.tril_indices(n)
+    for b in range(3):
+        Lref = np.linalg.cholesky(S[b])
+        ref = np.linalg.inv(Lref) if invert else Lref
+        np.testing.assert_allclose(A[b].cpu().numpy()[il], ref[il], rtol=1e-9,
+                                   atol=1e-10 * np.abs(ref).max())
+        np.testing.assert_array_equal(np.triu(A[b].cpu().numpy(), 1), np.triu(S[b], 1))
+        np.testing.assert_allclose(ld[b].cpu().numpy(), np.diag(Lref), rtol=1e-12)
+
+
+@pytest.mark.parametrize("ta,tb,tri_a,tri_b,lower", [(0, 0, 0, 0, 0), (1, 0, 1, 1, 0),
+                                                     (0, 1, 0, 0, 1), (0, 0, 1, 0, 0),
+                                                     (1, 1, 0, 0, 0)])
+@pytest.mark.parametrize("m,n,k", [(512, 512, 512), (130, 257, 300), (64, 96, 2048)])
+def test_gemm_batched(L, ta, tb, tri_a, tri_b, lower, m, n, k):
+    if lower:
+        n = m
+    if tri_a:
+        k = m
+    if tri_b:
+        k = n
+    rng = np.random.default_rng(m + n + k + 5 * ta + 7 * tb + 11 * tri_a)
+    nb = 3
+    A = rng.standard_normal((nb, k, m) if ta else (nb, m, k))
+    B = rng.standard_normal((nb, n, k) if tb else (nb, k, n))
+    C0 = rng.standard_normal((nb, m, n))
+    C = L.as_device(C0.copy())
+    L.gemm_batched(A, B, C, alpha=0.5, beta=-1.0, transa=bool(ta), transb=bool(tb),
+                   lower_c=bool(lower), tri_a=bool(tri_a), tri_b=bool(tri_b))
+    Ch = C.cpu().numpy()
+    for b in range(nb):
+        opA = np.swapaxes(A[b], 0, 1) if ta else A[b]
+        opB = np.swapaxes(B[b], 0, 1) if tb else B[b]
+        if tri_a:
+            opA = np.tril(A[b]).T if ta else np.tril(A[b])
+        if tri_b:
+            opB = np.tril(B[b]).T if tb else np.tril(B[b])
+        ref = 0.5 * opA @ opB - C0[b]
+        if lower:
+            il = np.tril_indices(m)
+            np.testing.assert_allclose(Ch[b][il], ref[il], rtol=1e-11, atol=1e-10)
+            np.testing.assert_array_equal(Ch[b][np.triu_indices(m, 1)],
+                                          C0[b][np.triu_indices(m, 1)])
+        else:
+            np.testing.assert_allclose(Ch[b], ref, rtol=1e-11, atol=1e-10)
+
+
+@pytest.mark.parametrize("kind", ["eq", "matern52"])
+@pytest.mark.parametrize("n1,n2,d", [(512, 5000, 3), (37, 129, 5), (1, 1, 1)])
+def test_kernel_matrix_matvec(L, kind, n1, n2, d):
+    """Fused K(X1, X2) assembly + K v (the VGP's Kzx and c = Kzx y in one pass)."""
+    import torch
+    rng = np.random.default_rng(n1 + n2)
+    X1 = rng.uniform(-2, 2, (n1, d))
+    X2 = rng.uniform(-2, 2, (n2, d))
+    v = rng.standard_normal(n2)
+    K = torch.empty((n1, n2), dtype=torch.float64, device="cuda")
+    out = torch.empty(n1, dtype=torch.float64, device="cuda")
+    L.kernel_matrix_matvec(kind, X1, X2, 0.8, 0.9, v, K, out)
+    ref = ogp.kernel_matrix(kind, X1, X2, 0.8, 0.9)[0]
+    np.testing.assert_allclose(K.cpu().numpy(), ref, rtol=1e-13, atol=1e-300)
+    np.testing.assert_allclose(out.cpu().numpy(), ref @ v, rtol=1e-11, atol=1e-12)

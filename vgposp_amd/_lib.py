@@ -62,6 +62,10 @@ SIGNATURES = {
     "vgposp_gemm": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p, _i64,
                            _f64, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p]),
     "vgposp_gemm_splitk_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32]),
+    "vgposp_gemm_batched_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32]),
+    "vgposp_gemm_batched": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _i64,
+                                   _c_void_p, _i64, _i64, _f64, _c_void_p, _i64, _i64, _i32, _i32,
+                                   _i32, _i32, _c_void_p, _size, _c_void_p]),
     "vgposp_gemm_splitk": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p,
                                   _i64, _f64, _c_void_p, _i64, _i32, _i32, _i32, _i32, _c_void_p,
                                   _size, _c_void_p]),
@@ -69,8 +73,8 @@ SIGNATURES = {
     "vgposp_kernel_matrix_matvec": (_i32, [_i32, _c_void_p, _i64, _c_void_p, _i64, _i32,
                                            _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
                                            _c_void_p, _c_void_p, _size, _c_void_p]),
-    "vgposp_vgp_sinv": (_i32, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _f64, _c_void_p,
-                               _c_void_p]),
+    "vgposp_vgp_sinv": (_i32, [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _f64, _f64, _c_void_p,
+                               _i32, _c_void_p]),
     "vgposp_sym_from_lower": (_i32, [_c_void_p, _i64, _i64, _c_void_p]),
     "vgposp_lincomb": (_i32, [_i64, _i64, _i64, _i32, _c_void_p, _c_void_p, _c_void_p, _f64, _f64,
                               _i32, _c_void_p, _f64, _c_void_p, _c_void_p]),
@@ -90,6 +94,7 @@ SIGNATURES = {
     "vgposp_center_rows": (_i32, [_c_void_p, _i64, _i64, _i64, _f64, _c_void_p]),
     "vgposp_index_taper": (_i32, [_c_void_p, _i64, _i64, _i64, _i64, _i64, _f64, _f64, _i32,
                                   _c_void_p]),
+    "vgposp_potrf_batched_workspace_bytes": (_size, [_i64, _i32]),
     "vgposp_potrf_workspace_bytes": (_size, [_i64]),
     "vgposp_potrf_lower": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _c_void_p, _c_void_p,
                                   _c_void_p, _size, _c_void_p]),

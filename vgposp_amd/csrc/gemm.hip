@@ -48,6 +48,9 @@ struct GemmParams {
   int nsplit, nblk;
   int64_t kchunk;
   double* part;
+  // batch (grid.y of the fast kernel, grid.z of the reference kernel): element b reads
+  // A + b sA, B + b sB and writes C + b sC (split-K partials at part + b sP)
+  int64_t sA, sB, sC, sP;
 };
 
 // Stage one operand tile (128 rows of the M/N dimension x 16 of K) into registers.
@@ -134,6 +137,9 @@ __global__ __launch_bounds__(256) void gemm_ref_kernel(GemmParams p, int vec_a, 
   const int64_t m0 = (int64_t)blockIdx.y * GBM;
   const int64_t n0 = (int64_t)blockIdx.x * GBN;
   if (p.uplo_c == VGPOSP_LOWER && n0 > m0 + GBM - 1) return;  // tile entirely above diagonal
+  p.A += blockIdx.z * p.sA;
+  p.B += blockIdx.z * p.sB;
+  p.C += blockIdx.z * p.sC;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -341,6 +347,9 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     if (TRIA && !TA) ti = tiles_m - 1 - ti;  // longest K ranges first
   }
   const int64_t m0 = (int64_t)ti * TBM, n0 = (int64_t)tj * GBN;
+  const int64_t bz = blockIdx.y;  // batch element
+  const double* const gA = p.A + bz * p.sA;
+  const double* const gB = p.B + bz * p.sB;
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -380,9 +389,9 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     const int64_t k0 = kbeg + (int64_t)t * GBK;
     const int op = q / PO, j = wave * PO + q % PO;
     if (op < NSUB)
-      glds_piece<A_KC>(p.A, p.lda, m0 + GBM * op, k0, p.m, p.k, st + op * OPND_ELEMS, j, lane);
+      glds_piece<A_KC>(gA, p.lda, m0 + GBM * op, k0, p.m, p.k, st + op * OPND_ELEMS, j, lane);
     else
-      glds_piece<B_KC>(p.B, p.ldb, n0, k0, p.n, p.k, st + NSUB * OPND_ELEMS, j, lane);
+      glds_piece<B_KC>(gB, p.ldb, n0, k0, p.n, p.k, st + NSUB * OPND_ELEMS, j, lane);
   };
   auto issue = [&](int t) {
 #pragma unroll
@@ -474,10 +483,10 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
         const int64_t row = m0 + wm * WROWS + (A_IL ? 32 * (i >> 1) + 2 * x + (i & 1) : i * 16 + x);
         if (row < p.m && col < p.n && (!lower || col <= row)) {
           if (p.nsplit > 1) {
-            p.part[(int64_t)zsplit * p.m * p.n + row * p.n + col] = p.alpha * acc[i][j][r];
+            p.part[bz * p.sP + (int64_t)zsplit * p.m * p.n + row * p.n + col] = p.alpha * acc[i][j][r];
             continue;
           }
-          double* c = p.C + row * p.ldc + col;
+          double* c = p.C + bz * p.sC + row * p.ldc + col;
           double v = p.alpha * acc[i][j][r];
           if (p.beta != 0.0) v += p.beta * *c;
           *c = v;
@@ -517,9 +526,12 @@ static void launch_glds(dim3 g1, hipStream_t stream, const GemmParams& p, int tm
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int64_t m, int64_t n, int nsplit,
                                                                  const double* part, double beta,
                                                                  double* C, int64_t ldc,
-                                                                 int lower) {
+                                                                 int lower, int64_t sP = 0,
+                                                                 int64_t sC = 0) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= m * n) return;
+  part += blockIdx.y * sP;
+  C += blockIdx.y * sC;
   const int64_t row = e / n, col = e - row * n;
   if (lower && col > row) return;
   double v = 0.0;
@@ -629,11 +641,21 @@ static bool aligned16(const void* ptr, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(ptr) % 16 == 0) && (ld % 2 == 0);
 }
 
-int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
-                      const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
-                      double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
-                      double* part, hipStream_t stream) {
-  if (m <= 0 || n <= 0) return 0;
+int gemm_launch_batched(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                        const double* A, int64_t lda, int64_t sA, const double* B, int64_t ldb,
+                        int64_t sB, double beta, double* C, int64_t ldc, int64_t sC, int uplo_c,
+                        int tri_a, int tri_b, int nsplit, double* part, int64_t sP, int batch,
+                        hipStream_t stream) {
+  if (m <= 0 || n <= 0 || batch <= 0) return 0;
+  if (n == 1 && !tri_b && uplo_c == VGPOSP_FULL && k > 0 && batch > 1) {
+    for (int b = 0; b < batch; ++b) {
+      int rc = gemm_launch_batched(transa, transb, m, n, k, alpha, A + b * sA, lda, 0, B + b * sB,
+                                   ldb, 0, beta, C + b * sC, ldc, 0, uplo_c, tri_a, tri_b, nsplit,
+                                   part ? part + b * sP : nullptr, 0, 1, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   if (n == 1 && !tri_b && uplo_c == VGPOSP_FULL && k > 0) {
     ProfScope ps("gemv_f64", stream, 2.0 * (double)m * k, 8.0 * ((double)m * k + k + 2.0 * m));
     const int64_t incx = transb ? 1 : ldb;
@@ -660,15 +682,17 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
     }
     return 0;
   }
-  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr};
-  const int va = aligned16(A, lda), vb = aligned16(B, ldb);
+  GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr,
+               sA, sB, sC, sP};
+  const int va = aligned16(A, lda) && (batch == 1 || sA % 2 == 0);
+  const int vb = aligned16(B, ldb) && (batch == 1 || sB % 2 == 0);
   const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
   if (va && vb && even) {
     const int tm = (int)ceil_div(m, GBM), tn = (int)ceil_div(n, GBN);
     const int64_t nblk = (uplo_c == VGPOSP_LOWER) ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
     const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
     // algorithmic flops: a triangular operand halves the useful products
-    const double fl = 2.0 * (double)k * outs * ((tri_a && tri_b) ? (1.0 / 3.0) : (tri_a || tri_b) ? 0.5 : 1.0);
+    const double fl = 2.0 * batch * (double)k * outs * ((tri_a && tri_b) ? (1.0 / 3.0) : (tri_a || tri_b) ? 0.5 : 1.0);
     if (nsplit > 1 && part != nullptr) {
       p.nblk = (int)nblk;
       p.kchunk = ceil_div(ceil_div(k, nsplit), GBK) * GBK;
@@ -676,27 +700,36 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
       p.part = part;
     }
     ProfScope ps("gemm_f64", stream, fl,
-                 8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
-    dim3 g1((unsigned)(nblk * p.nsplit));
+                 8.0 * batch * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    dim3 g1((unsigned)(nblk * p.nsplit), (unsigned)batch);
     launch_glds<1>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     VG_LAUNCH_CHECK();
     if (p.nsplit > 1) {
-      hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(m * n, 256)), dim3(256),
-                         0, stream, m, n, p.nsplit, part, beta, C, ldc, uplo_c == VGPOSP_LOWER);
+      hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)ceil_div(m * n, 256), (unsigned)batch),
+                         dim3(256), 0, stream, m, n, p.nsplit, part, beta, C, ldc,
+                         uplo_c == VGPOSP_LOWER, sP, sC);
       VG_LAUNCH_CHECK();
     }
     return 0;
   }
-  dim3 grid((unsigned)ceil_div(n, GBN), (unsigned)ceil_div(m, GBM));
+  dim3 grid((unsigned)ceil_div(n, GBN), (unsigned)ceil_div(m, GBM), (unsigned)batch);
   const double outs = (uplo_c == VGPOSP_LOWER) ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
-  ProfScope ps("gemm_f64", stream, 2.0 * (double)k * outs,
-               8.0 * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+  ProfScope ps("gemm_f64", stream, 2.0 * batch * (double)k * outs,
+               8.0 * batch * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
   if (!transa && !transb) hipLaunchKernelGGL((gemm_ref_kernel<false, false>), grid, dim3(256), 0, stream, p, va, vb);
   else if (!transa && transb) hipLaunchKernelGGL((gemm_ref_kernel<false, true>), grid, dim3(256), 0, stream, p, va, vb);
   else if (transa && !transb) hipLaunchKernelGGL((gemm_ref_kernel<true, false>), grid, dim3(256), 0, stream, p, va, vb);
   else hipLaunchKernelGGL((gemm_ref_kernel<true, true>), grid, dim3(256), 0, stream, p, va, vb);
   VG_LAUNCH_CHECK();
   return 0;
+}
+
+int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                      const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                      double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
+                      double* part, hipStream_t stream) {
+  return gemm_launch_batched(transa, transb, m, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0,
+                             uplo_c, tri_a, tri_b, nsplit, part, 0, 1, stream);
 }
 
 int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
@@ -789,4 +822,38 @@ extern "C" int vgposp_gemm(int transa, int transb, int64_t m, int64_t n, int64_t
   VG_CHECK_ARG(uplo_c == VGPOSP_FULL || (uplo_c == VGPOSP_LOWER && m == n), 14);
   return gemm_launch(transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, uplo_c, tri_a,
                      tri_b, as_stream(stream));
+}
+
+extern "C" size_t vgposp_gemm_batched_workspace_bytes(int64_t m, int64_t n, int64_t k, int uplo_c,
+                                                      int batch) {
+  using namespace vgposp;
+  if (m <= 0 || n <= 0 || k <= 0 || batch <= 0 || n == 1) return 0;
+  const int sp = auto_splits(m, n, k, uplo_c, 0);
+  return sp > 1 ? 8 * (size_t)sp * m * n * batch : 0;
+}
+
+extern "C" int vgposp_gemm_batched(int transa, int transb, int64_t m, int64_t n, int64_t k,
+                                   double alpha, const double* A, int64_t lda, int64_t sA,
+                                   const double* B, int64_t ldb, int64_t sB, double beta, double* C,
+                                   int64_t ldc, int64_t sC, int uplo_c, int tri_a, int tri_b,
+                                   int batch, void* ws, size_t ws_bytes, void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(m >= 0, 3);
+  VG_CHECK_ARG(n >= 0, 4);
+  VG_CHECK_ARG(k >= 0, 5);
+  VG_CHECK_ARG(A != nullptr || m == 0 || k == 0, 7);
+  VG_CHECK_ARG(lda >= (transa ? (m > 0 ? m : 1) : (k > 0 ? k : 1)), 8);
+  VG_CHECK_ARG(B != nullptr || n == 0 || k == 0, 10);
+  VG_CHECK_ARG(ldb >= (transb ? (k > 0 ? k : 1) : (n > 0 ? n : 1)), 11);
+  VG_CHECK_ARG(C != nullptr || m == 0 || n == 0, 14);
+  VG_CHECK_ARG(ldc >= (n > 0 ? n : 1), 15);
+  VG_CHECK_ARG(uplo_c == VGPOSP_FULL || (uplo_c == VGPOSP_LOWER && m == n), 17);
+  VG_CHECK_ARG(batch >= 1 && batch <= 65535, 20);
+  if (m == 0 || n == 0) return 0;
+  int sp = (k > 0 && n > 1) ? auto_splits(m, n, k, uplo_c, transa) : 1;
+  if (sp > 1 && (ws == nullptr || ws_bytes < 8 * (size_t)sp * m * n * batch)) sp = 1;
+  return gemm_launch_batched(transa, transb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc,
+                             sC, uplo_c, tri_a, tri_b, sp, sp > 1 ? static_cast<double*>(ws) : nullptr,
+                             (int64_t)sp * m * n, batch, as_stream(stream));
 }

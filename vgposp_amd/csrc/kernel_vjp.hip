@@ -13,40 +13,13 @@
 // the workspace ([col-blocks][n1][d] and [blocks][2]) and a second kernel reduces them in a fixed
 // order: results are deterministic.
 #include "common.h"
+#include "psd.h"
 
 namespace vgposp {
 
 constexpr int VJ_ROWS = 16;
 constexpr int VJ_COLS = 1024;
 constexpr int VJ_MAXD = 8;
-
-// K, dK/dls and the coefficient c with dK/dx1 = c * (x1 - x2), for one entry.
-template <int KIND>
-__device__ __forceinline__ void kvjp_entry(double d2, double tla, double inv_l, double inv_l2,
-                                           double& K, double& dkl, double& cx) {
-  if (KIND == VGPOSP_KERNEL_EQ) {
-    K = exp(tla - 0.5 * d2 * inv_l2);
-    dkl = K * d2 * inv_l2 * inv_l;
-    cx = -K * inv_l2;
-  } else if (KIND == VGPOSP_KERNEL_MATERN12) {
-    const double r = sqrt(d2) * inv_l;
-    K = exp(tla - r);
-    dkl = K * r * inv_l;
-    cx = r > 0.0 ? -K * inv_l2 / r : 0.0;  // direction undefined at r = 0: sub-gradient 0
-  } else if (KIND == VGPOSP_KERNEL_MATERN32) {
-    const double s = 1.7320508075688772 * sqrt(d2) * inv_l;
-    const double E = exp(tla - s);
-    K = E * (1.0 + s);
-    dkl = E * s * s * inv_l;
-    cx = -3.0 * E * inv_l2;
-  } else {
-    const double s = 2.23606797749979 * sqrt(d2) * inv_l;
-    const double E = exp(tla - s);
-    K = E * (1.0 + s + s * s * (1.0 / 3.0));
-    dkl = E * (s * s * (1.0 / 3.0)) * (1.0 + s) * inv_l;
-    cx = -(5.0 / 3.0) * (1.0 + s) * E * inv_l2;
-  }
-}
 
 template <int KIND, int D>
 __global__ __launch_bounds__(256) void kernel_vjp_kernel(const double* X1, int64_t n1,
@@ -119,34 +92,48 @@ __global__ __launch_bounds__(256) void kernel_vjp_kernel(const double* X1, int64
   }
 }
 
-// X1bar[i][k] = sum over column blocks (fixed order); block 0 also reduces the two scalars.
+// X1bar[i][k] = sum over the column blocks of part_x[cb][i][k]: one wave per output, lanes stride
+// over the blocks, fixed order (deterministic).  The last workgroup also reduces the two scalars.
 __global__ __launch_bounds__(256) void kernel_vjp_reduce_kernel(int64_t n1, int d, int64_t ncb,
                                                                 int64_t nblk, const double* part_x,
                                                                 const double* part_g,
                                                                 double* grad, double* X1bar) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (X1bar && e < n1 * d) {
-    double s = 0.0;
-    for (int64_t cb = 0; cb < ncb; ++cb) s += part_x[cb * n1 * d + e];
-    X1bar[e] = s;
-  }
-  if (blockIdx.x == 0) {
-    __shared__ double sh[2][4];
-    double s0 = 0.0, s1 = 0.0;
-    for (int64_t b = threadIdx.x; b < nblk; b += 256) {
-      s0 += part_g[2 * b];
-      s1 += part_g[2 * b + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nout = X1bar ? n1 * d : 0;
+  const int64_t nwg_x = (nout + 3) / 4;
+  if ((int64_t)blockIdx.x < nwg_x) {
+    const int64_t e = (int64_t)blockIdx.x * 4 + wv;
+    if (e < nout) {
+      double s = 0.0;
+      for (int64_t cb = lane; cb < ncb; cb += 64) s += part_x[cb * n1 * d + e];
+      s = wave_sum(s);
+      if (lane == 0) X1bar[e] = s;
     }
-    s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      sh[0][wv] = s0;
-      sh[1][wv] = s1;
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) grad[threadIdx.x] = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
+    return;
   }
+  __shared__ double sh[2][4];
+  double s0 = 0.0, s1 = 0.0;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) {
+    s0 += part_g[2 * b];
+    s1 += part_g[2 * b + 1];
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  if (lane == 0) {
+    sh[0][wv] = s0;
+    sh[1][wv] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) grad[threadIdx.x] = sh[threadIdx.x][0] + sh[threadIdx.x][1] + sh[threadIdx.x][2] + sh[threadIdx.x][3];
+}
+
+int kernel_vjp_reduce_launch(int64_t n1, int d, int64_t ncb, int64_t nblk, const double* part_x,
+                             const double* part_g, double* grad, double* X1bar, hipStream_t s) {
+  const int64_t nwg_x = X1bar ? ceil_div(n1 * d, 4) : 0;
+  hipLaunchKernelGGL(kernel_vjp_reduce_kernel, dim3((unsigned)(nwg_x + 1)), dim3(256), 0, s, n1, d,
+                     ncb, nblk, part_x, part_g, grad, X1bar);
+  VG_LAUNCH_CHECK();
+  return 0;
 }
 
 static void vjp_layout(int64_t n1, int64_t n2, int d, int64_t* ncb, int64_t* nrb, size_t* bytes) {
@@ -223,9 +210,5 @@ extern "C" int vgposp_kernel_vjp(int kind, const double* X1, int64_t n1, const d
     }
     VG_LAUNCH_CHECK();
   }
-  const int64_t nr = X1bar ? n1 * d : 1;
-  hipLaunchKernelGGL(kernel_vjp_reduce_kernel, dim3((unsigned)ceil_div(nr, 256)), dim3(256), 0, s,
-                     n1, d, ncb, ncb * nrb, px, pg, grad, X1bar);
-  VG_LAUNCH_CHECK();
-  return 0;
+  return kernel_vjp_reduce_launch(n1, d, ncb, ncb * nrb, px, pg, grad, X1bar, s);
 }

@@ -25,6 +25,11 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
                       double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
                       double* part, hipStream_t stream);
 int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa);
+int gemm_launch_batched(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
+                        const double* A, int64_t lda, int64_t sA, const double* B, int64_t ldb,
+                        int64_t sB, double beta, double* C, int64_t ldc, int64_t sC, int uplo_c,
+                        int tri_a, int tri_b, int nsplit, double* part, int64_t sP, int batch,
+                        hipStream_t stream);
 
 constexpr int NB = 128;        // leaf size (== GEMM tile, so trsm leaves are in place)
 
@@ -126,7 +131,9 @@ __device__ __forceinline__ void leaf_panel(double (&D0)[LW], double (&D1)[LW], i
 __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int64_t lda, int jb,
                                                                   int64_t col0, int invert,
                                                                   double* linv, double* diag_out,
-                                                                  int* info, int64_t stride_a) {
+                                                                  int* info, int64_t stride_a,
+                                                                  int64_t stride_linv = NB * NB,
+                                                                  int64_t stride_diag = -1) {
   extern __shared__ double L[];  // [NB][LP2]
   __shared__ double rdiag[NB];
   __shared__ double XD[(NB / LW) * LW * LW];  // dense diagonal blocks of L^-1
@@ -137,8 +144,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   const bool factor = invert != 2;
   A += blockIdx.x * stride_a;
   info += blockIdx.x;
-  if (linv) linv += (int64_t)blockIdx.x * NB * NB;
-  if (diag_out) diag_out += (int64_t)blockIdx.x * jb;
+  if (linv) linv += (int64_t)blockIdx.x * stride_linv;
+  if (diag_out) diag_out += (int64_t)blockIdx.x * (stride_diag < 0 ? jb : stride_diag);
   const int JP = (jb + LW - 1) & ~(LW - 1), NP = JP / LW;
   for (int e = t; e < NB * NB; e += LEAF_THREADS) {
     const int r = e / NB, c = e % NB;
@@ -291,9 +298,12 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
 
 static size_t leaf_shmem() { return (size_t)NB * LP2 * sizeof(double); }
 
-// A (jb x jb lower) <- linv (the saved leaf inverse)
-__global__ void copy_leaf_kernel(double* A, int64_t lda, int jb, const double* linv) {
+// A (jb x jb lower) <- linv (the saved leaf inverse); batch element blockIdx.y at the strides
+__global__ void copy_leaf_kernel(double* A, int64_t lda, int jb, const double* linv,
+                                 int64_t sA = 0, int64_t sL = 0) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  A += blockIdx.y * sA;
+  linv += blockIdx.y * sL;
   const int r = e / NB, c = e % NB;
   if (r < jb && c <= r) A[(int64_t)r * lda + c] = linv[e];
 }
@@ -319,8 +329,18 @@ struct Fact {
   int* info;
   double* part;      // split-K partials, PART_ELEMS doubles (or null)
   hipStream_t s;
+  int64_t diag_n = 0;  // batched: diag_out stride (the matrix order)
+  // batched recursion: `batch` matrices at stride sA, each with its own copy of the workspace
+  // (stride sW doubles from ws0); a pointer into [ws0, ws0 + sW) is a workspace operand
+  int batch = 1;
+  int64_t sA = 0, sW = 0;
+  const double* ws0 = nullptr;
   double* leaf(int64_t col0) const { return linv_all + (col0 / NB) * NB * NB; }
   double* xblk(int64_t col0) const { return xinv + col0 * NBI; }
+  int64_t stride(const void* p) const {
+    const double* d = static_cast<const double*>(p);
+    return (ws0 && d >= ws0 && d < ws0 + sW) ? sW : sA;
+  }
 };
 
 // Split-K partials for the recursion's few-tile GEMMs (the 128..1024 levels: a 128^3 TRSM or SYRK
@@ -335,6 +355,10 @@ static int pgemm(const Fact& f, int transa, int transb, int64_t m, int64_t n, in
                  double beta, double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b) {
   int sp = f.part ? gemm_auto_splits(m, n, k, uplo_c, transa) : 1;
   while (sp > 1 && (int64_t)sp * m * n > PART_ELEMS) --sp;
+  if (f.batch > 1)
+    return gemm_launch_batched(transa, transb, m, n, k, alpha, A, lda, f.stride(A), B, ldb,
+                               f.stride(B), beta, C, ldc, f.stride(C), uplo_c, tri_a, tri_b, sp,
+                               sp > 1 ? f.part : nullptr, f.sW, f.batch, f.s);
   return gemm_launch_split(transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, uplo_c,
                            tri_a, tri_b, sp, sp > 1 ? f.part : nullptr, f.s);
 }
@@ -342,8 +366,10 @@ static int pgemm(const Fact& f, int transa, int transb, int64_t m, int64_t n, in
 // dst (n x n lower, ldd) <- src (lower, lds); zero_upper: also zero dst's strict upper triangle
 // (dst is then a full-matrix GEMM operand); otherwise dst's upper triangle is left untouched.
 __global__ void copy_lower_kernel(double* dst, int64_t ldd, const double* src, int64_t lds,
-                                  int64_t n, int zero_upper) {
+                                  int64_t n, int zero_upper, int64_t sd = 0, int64_t ss = 0) {
   const int64_t r = blockIdx.y;
+  dst += blockIdx.z * sd;
+  src += blockIdx.z * ss;
   for (int64_t c = threadIdx.x; c < n; c += blockDim.x) {
     if (c <= r) dst[r * ldd + c] = src[r * lds + c];
     else if (zero_upper) dst[r * ldd + c] = 0.0;
@@ -352,17 +378,20 @@ __global__ void copy_lower_kernel(double* dst, int64_t ldd, const double* src, i
 
 static int copy_lower(const Fact& f, double* dst, int64_t ldd, const double* src, int64_t lds,
                       int64_t n, int zero_upper) {
-  hipLaunchKernelGGL(copy_lower_kernel, dim3(1, (unsigned)n), dim3(256), 0, f.s, dst, ldd, src, lds,
-                     n, zero_upper);
+  hipLaunchKernelGGL(copy_lower_kernel, dim3(1, (unsigned)n, (unsigned)f.batch), dim3(256), 0, f.s,
+                     dst, ldd, src, lds, n, zero_upper, f.stride(dst), f.stride(src));
   VG_LAUNCH_CHECK();
   return 0;
 }
 
 static int leaf_factor(const Fact& f, double* A, int jb, int64_t col0, int invert) {
-  ProfScope ps("potrf_diag", f.s, 2.0 * jb * (double)jb * jb / 3.0, 8.0 * jb * (double)jb * 2);
-  hipLaunchKernelGGL(potrf_leaf_kernel, dim3(1), dim3(LEAF_THREADS), leaf_shmem(), f.s, A, f.lda,
-                     jb, col0, invert, f.leaf(col0), f.diag_out ? f.diag_out + col0 : nullptr,
-                     f.info, (int64_t)0);
+  ProfScope ps("potrf_diag", f.s, f.batch * 2.0 * jb * (double)jb * jb / 3.0,
+               f.batch * 8.0 * jb * (double)jb * 2);
+  // batched: one workgroup per matrix; element b's status is info[b], its diagonal diag_out + b n
+  hipLaunchKernelGGL(potrf_leaf_kernel, dim3((unsigned)f.batch), dim3(LEAF_THREADS), leaf_shmem(),
+                     f.s, A, f.lda, jb, col0, invert, f.leaf(col0),
+                     f.diag_out ? f.diag_out + col0 : nullptr, f.info, f.sA, f.sW,
+                     f.batch > 1 ? f.diag_n : (int64_t)-1);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -382,8 +411,10 @@ static int trsm_rec(const Fact& f, double* B, int64_t m, int64_t ldb, const doub
     if ((rc = pgemm(f, 0, 1, m, nL, nL, 1.0, B, ldb, f.xblk(col0), NBI, 0.0, f.tmp, NBI,
                     VGPOSP_FULL, 0, 1)))
       return rc;
-    VG_HIP(hipMemcpy2DAsync(B, ldb * sizeof(double), f.tmp, NBI * sizeof(double),
-                            nL * sizeof(double), m, hipMemcpyDeviceToDevice, f.s));
+    for (int b = 0; b < f.batch; ++b)
+      VG_HIP(hipMemcpy2DAsync(B + b * f.stride(B), ldb * sizeof(double), f.tmp + b * f.sW,
+                              NBI * sizeof(double), nL * sizeof(double), m,
+                              hipMemcpyDeviceToDevice, f.s));
     return 0;
   }
   const int64_t a = split_point(nL), b = nL - a;
@@ -400,8 +431,8 @@ static int trsm_rec(const Fact& f, double* B, int64_t m, int64_t ldb, const doub
 static int trtri_rec(const Fact& f, double* A, int64_t lda, int64_t n, int64_t col0, bool blocks) {
   if (n <= NB) {
     ProfScope ps("trtri_leaf", f.s, 0.0, 8.0 * NB * NB * 2);
-    hipLaunchKernelGGL(copy_leaf_kernel, dim3(NB * NB / 256), dim3(256), 0, f.s, A, lda, (int)n,
-                       f.leaf(col0));
+    hipLaunchKernelGGL(copy_leaf_kernel, dim3(NB * NB / 256, (unsigned)f.batch), dim3(256), 0, f.s,
+                       A, lda, (int)n, f.leaf(col0), f.stride(A), f.sW);
     VG_LAUNCH_CHECK();
     return 0;
   }
@@ -473,6 +504,25 @@ static Fact make_fact(int64_t n, int64_t lda, void* ws, double* diag_out, int* i
   double* tmp = blocks ? xinv + n * NBI : nullptr;
   double* part = n > NB ? work + n1 * (n - n1) + (blocks ? 2 * n * NBI : 0) : nullptr;
   return Fact{lda, base, work, xinv, tmp, diag_out, info, part, stream};
+}
+
+// `batch` matrices at stride sA factored by ONE recursion: every launch covers all of them (the
+// leaves as one workgroup per matrix, the GEMMs with a batch grid dimension), so B small
+// factorizations cost the launches and the latency chain of one.  ws holds B copies of the
+// single-matrix workspace.
+int potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int batch, int invert,
+                  double* diag_out, int* info, void* ws, hipStream_t stream) {
+  if (int rc = ensure_leaf_attr()) return rc;
+  const bool blocks = n > NBI;
+  Fact f = make_fact(n, lda, ws, diag_out, info, stream);
+  f.batch = batch;
+  f.sA = sA;
+  f.sW = (int64_t)(potrf_ws_bytes(n) / sizeof(double));
+  f.ws0 = static_cast<const double*>(ws);
+  f.diag_n = n;
+  int rc = potrf_rec(f, A, n, 0, blocks);
+  if (rc || !invert) return rc;
+  return trtri_rec(f, A, lda, n, 0, blocks);
 }
 
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
@@ -694,6 +744,10 @@ extern "C" size_t vgposp_potrf_workspace_bytes(int64_t n) {
   return n > 0 ? vgposp::potrf_ws_bytes(n) : 0;
 }
 
+extern "C" size_t vgposp_potrf_batched_workspace_bytes(int64_t n, int batch) {
+  return n > 0 && batch > 0 ? (size_t)batch * vgposp::potrf_ws_bytes(n) : 0;
+}
+
 extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t stride, int batch,
                                   int invert, double* diag_out, int* info, void* ws,
                                   size_t ws_bytes, void* stream) {
@@ -727,6 +781,8 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
     VG_LAUNCH_CHECK();
     return 0;
   }
+  if (batch > 1 && ws_bytes >= (size_t)batch * potrf_ws_bytes(n))
+    return potrf_batched(A, n, lda, stride, batch, invert, diag_out, info, ws, s);
   for (int b = 0; b < batch; ++b) {
     int rc = potrf_one(A + b * stride, n, lda, invert, diag_out ? diag_out + (int64_t)b * n : nullptr,
                        info + b, ws, s);

@@ -23,4 +23,32 @@ __device__ __forceinline__ double kfun(double d2, double two_log_amp, double inv
   return (1.0 + s + s * s * (1.0 / 3.0)) * exp(two_log_amp - s);
 }
 
+// K, dK/dls and the coefficient c with dK/dx1 = c * (x1 - x2), for one entry.
+template <int KIND>
+__device__ __forceinline__ void kvjp_entry(double d2, double tla, double inv_l, double inv_l2,
+                                           double& K, double& dkl, double& cx) {
+  if (KIND == VGPOSP_KERNEL_EQ) {
+    K = exp(tla - 0.5 * d2 * inv_l2);
+    dkl = K * d2 * inv_l2 * inv_l;
+    cx = -K * inv_l2;
+  } else if (KIND == VGPOSP_KERNEL_MATERN12) {
+    const double r = sqrt(d2) * inv_l;
+    K = exp(tla - r);
+    dkl = K * r * inv_l;
+    cx = r > 0.0 ? -K * inv_l2 / r : 0.0;  // direction undefined at r = 0: sub-gradient 0
+  } else if (KIND == VGPOSP_KERNEL_MATERN32) {
+    const double s = 1.7320508075688772 * sqrt(d2) * inv_l;
+    const double E = exp(tla - s);
+    K = E * (1.0 + s);
+    dkl = E * s * s * inv_l;
+    cx = -3.0 * E * inv_l2;
+  } else {
+    const double s = 2.23606797749979 * sqrt(d2) * inv_l;
+    const double E = exp(tla - s);
+    K = E * (1.0 + s + s * s * (1.0 / 3.0));
+    dkl = E * (s * s * (1.0 / 3.0)) * (1.0 + s) * inv_l;
+    cx = -(5.0 / 3.0) * (1.0 + s) * E * inv_l2;
+  }
+}
+
 }  // namespace vgposp

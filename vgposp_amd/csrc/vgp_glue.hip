@@ -3,7 +3,8 @@
 // (variational_Gaussian_process_example.py:51-102) that is not a GEMM, a factorization, a kernel
 // assembly or a kernel VJP.  Each was a chain of small framework kernels (and one-element kernels
 // for every scalar); here each phase is one launch over M x M (or M) data that sits in L2:
-//   vgp_sinv     P0 (lower) -> symmetric in place, Sinv = Kzz + P0 / s + pj I
+//   vgp_sinv     P0 (lower) -> symmetric in place, Sinv = Kzz + P0 / s + pj I (+ the Kzz
+//                matrices factored in the same batch)
 //   sym_lower    A (lower) -> symmetric in place
 //   lincomb      out = sum_k c_k (s + shift)^e_k X_k  (+ a diagonal term), M x M or vectors
 //   vgp_kzz_bar  the adjoint of Kzz (symmetrised, as the Kzz VJP wants it) and G = (2/s) Sinv_bar
@@ -22,14 +23,21 @@ constexpr int MAX_TERMS = 4;
 
 __global__ __launch_bounds__(256) void vgp_sinv_kernel(int64_t n, double* P0, int64_t ld,
                                                        const double* Kzz, const double* s,
-                                                       double pj, double* Sinv) {
+                                                       double pj, double jitter, double* F,
+                                                       int nf) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= n * n) return;
   const int64_t i = e / n, j = e - i * n;
   const double p = j <= i ? P0[i * ld + j] : P0[j * ld + i];
-  double v = Kzz[i * n + j] + p / s[0];
+  const double k = Kzz[i * n + j];
+  double v = k + p / s[0];
   if (i == j) v += pj;
-  Sinv[i * n + j] = v;
+  F[e] = v;
+  if (nf == 4) {  // the three Kzz-only matrices the step factors in the same batch
+    F[n * n + e] = i == j ? k + jitter : k;
+    F[2 * n * n + e] = i == j ? k + (s[0] + 1e-6) : k;
+    F[3 * n * n + e] = k;
+  }
   if (j > i) P0[i * ld + j] = p;  // only the strict upper triangle is written, only lower read
 }
 
@@ -178,16 +186,18 @@ static dim3 grid1(int64_t n) { return dim3((unsigned)ceil_div(n, 256)); }
 using namespace vgposp;
 
 extern "C" int vgposp_vgp_sinv(double* P0, int64_t n, int64_t ldp, const double* Kzz,
-                               const double* s, double pj, double* Sinv, void* stream) {
+                               const double* s, double pj, double jitter, double* F, int nf,
+                               void* stream) {
   clear_error();
   VG_CHECK_ARG(P0 != nullptr, 1);
   VG_CHECK_ARG(n >= 1, 2);
   VG_CHECK_ARG(ldp >= n, 3);
   VG_CHECK_ARG(Kzz != nullptr, 4);
   VG_CHECK_ARG(s != nullptr, 5);
-  VG_CHECK_ARG(Sinv != nullptr, 7);
+  VG_CHECK_ARG(F != nullptr, 8);
+  VG_CHECK_ARG(nf == 1 || nf == 4, 9);
   hipLaunchKernelGGL(vgp_sinv_kernel, grid1(n * n), dim3(256), 0, as_stream(stream), n, P0, ldp, Kzz,
-                     s, pj, Sinv);
+                     s, pj, jitter, F, nf);
   VG_LAUNCH_CHECK();
   return 0;
 }

@@ -142,6 +142,29 @@ def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=
     return C
 
 
+def gemm_batched(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=False,
+                 tri_a=False, tri_b=False):
+    """C[b] = alpha op(A[b]) op(B[b]) + beta C[b] for [batch, rows, cols] contiguous operands, one
+    launch (vgposp_gemm_batched, split-K when few output tiles)."""
+    A, B = as_device(A), as_device(B)
+    nb = A.shape[0]
+    m = A.shape[2] if transa else A.shape[1]
+    k = A.shape[1] if transa else A.shape[2]
+    n = B.shape[1] if transb else B.shape[2]
+    if B.shape[0] != nb or (B.shape[2] if transb else B.shape[1]) != k:
+        raise ValueError("gemm_batched: shapes do not match")
+    if C is None:
+        C = (torch.zeros if lower_c else torch.empty)((nb, m, n), dtype=F64, device=A.device)
+        beta = 0.0
+    uplo = LOWER if lower_c else FULL
+    ws = workspace(query("vgposp_gemm_batched_workspace_bytes", m, n, k, uplo, nb))
+    call("vgposp_gemm_batched", int(transa), int(transb), m, n, k, float(alpha), _p(A),
+         A.stride(1), A.stride(0), _p(B), B.stride(1), B.stride(0), float(beta), _p(C),
+         C.stride(1), C.stride(0), uplo, int(tri_a), int(tri_b), nb, _p(ws), ws.numel(),
+         _stream())
+    return C
+
+
 def _batched(A):
     if A.dim() == 2:
         return A.unsqueeze(0), True
@@ -168,7 +191,9 @@ def cholesky_(A, invert=False, check=True, ldiag=None):
     if ldiag is None:
         ldiag = torch.empty((Bn, n), dtype=F64, device=A3.device)
     info = torch.empty(Bn, dtype=torch.int32, device=A3.device)
-    ws = workspace(query("vgposp_potrf_workspace_bytes", n))
+    # a batch of n > 128 matrices runs as ONE recursion (every launch covers the batch)
+    ws = workspace(query("vgposp_potrf_batched_workspace_bytes", n, Bn) if Bn > 1 and n > 128
+                   else query("vgposp_potrf_workspace_bytes", n))
     call("vgposp_potrf_lower", _p(A3), n, A3.stride(1), A3.stride(0), Bn, int(invert), _p(ldiag),
          _p(info), _p(ws), ws.numel(), _stream())
     if check:
