@@ -188,3 +188,32 @@ def test_gemv_split_and_transposed(torch_dev, m, k, transa):
                 beta=-2.0, transa=transa)
     ref = 0.5 * ((A.T if transa else A) @ x) - 2.0 * y0
     np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-11, atol=1e-10)
+
+
+@pytest.mark.parametrize("n", [24, 64])
+def test_graph_replays_match_eager(torch_dev, n):
+    """Many back-to-back HIP-graph replays of the VGP training step (bench.py's loop shape: feeds
+    indexed on device, no host read between steps) give bit-identical losses to the eager step.
+    n = 64 is config C3, where the 10th replay once read a corrupted status before the replay
+    was synchronised (tools/repro_vgp2.py)."""
+    import os
+
+    from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
+    torch = torch_dev
+    X, y, Z = vgp_c3_data(n=n)
+    N = len(X)
+    B = N // 8
+    rng = np.random.default_rng(1)
+    idx = [torch.as_tensor(rng.integers(0, N, B), device="cuda") for _ in range(14)]
+    losses = {}
+    for mode in ("1", "0"):
+        os.environ["VGPOSP_GRAPH"] = mode
+        try:
+            train_op, _, xb, yb = vgp_c3_graph(X, y, Z, B)
+            Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
+            out = [train_op.run({xb: Xd[i], yb: yd[i]}) for i in idx]
+            losses[mode] = [float(v) for v in out]
+            assert bool(train_op.graph) == (mode == "1")
+        finally:
+            os.environ.pop("VGPOSP_GRAPH", None)
+    assert losses["1"] == losses["0"]

@@ -211,6 +211,11 @@ class VGPTrainOp:
         sX.copy_(Xb)
         sy.copy_(yb)
         g.replay()
+        # Wait for the replay on the host before reading its status.  Measured on this ROCm
+        # build: without the explicit stream sync the 10th back-to-back replay of this graph read
+        # corrupted statuses (tools/repro_vgp2.py); with it, every replay is bit-identical to the
+        # eager step.  The step already synchronised once per run through the status check.
+        torch.cuda.current_stream().synchronize()
         linalg.check_info(status)
         return loss.clone()
 
