@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--c4-steps", type=int, default=10)
     p.add_argument("--no-splits", action="store_true",
                    help="skip the N > 1 independent-splits extra")
+    p.add_argument("--backend", default="nccl",
+                   help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
+                        "the multi-rank path on one GPU with VGPOSP_BENCH_DEVICE=0)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r1.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
@@ -204,10 +207,11 @@ def vgp_line(args, which="c3", precision="fp64"):
                      "launches_per_step": n, "note": "one eager step with event timing"}}
 
 
-def c2_line(reps=2):
+def c2_line(reps=5):
     """Config C2: N = 32,768 (32^3 grid) K assembly (lower triangle + noise on the
     diagonal, GB/s of algorithmic bytes 4 n (n + 1) + 8 d n) and the fp64 Cholesky (GF/s of
-    n^3 / 3), each the best of ``reps`` runs after a warm-up."""
+    n^3 / 3), each the best of ``reps`` runs after a warm-up.  The kernel parameters are device
+    tensors made once, so no host-to-device copy sits inside the timed region."""
     import torch
 
     from vgposp_amd import linalg
@@ -218,10 +222,12 @@ def c2_line(reps=2):
     A = torch.empty((1, n, n), dtype=torch.float64, device="cuda")
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
-    def assemble():
-        linalg.kernel_matrix("eq", Xd, None, 1.0, ls, diag_shift=0.01 + 1e-6, lower=True, out=A)
+    amp_d, ls_d, sh_d = (linalg.as_device([v]) for v in (1.0, ls, 0.01 + 1e-6))
 
-    def timed(fn):
+    def assemble():
+        linalg.kernel_matrix("eq", Xd, None, amp_d, ls_d, diag_shift=sh_d, lower=True, out=A)
+
+    def timed(fn, reps=reps):
         best = None
         for _ in range(reps):
             assemble()
@@ -237,7 +243,7 @@ def c2_line(reps=2):
     assemble()
     linalg.cholesky_(A[0], check=True)  # warm-up (and the PD check)
     t_k = timed(assemble)
-    t_c = timed(lambda: linalg.cholesky_(A[0], check=False))
+    t_c = timed(lambda: linalg.cholesky_(A[0], check=False), reps=2)
     del A
     torch.cuda.empty_cache()
     return {"config": {"workload": "C2: 32^3 grid over [-2,2]^3, EQ amp 1 ls 2h, noise 1e-2+1e-6",
@@ -335,9 +341,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    # VGPOSP_BENCH_DEVICE pins every rank to one device (rehearsing N > 1 on a one-GPU box)
+    dev = int(os.environ.get("VGPOSP_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.backend)
 
     from vgposp_amd import _lib, linalg
     from vgposp_amd.placement_algorithm2 import GreedyPlacement
@@ -351,7 +362,8 @@ def main():
     def maxtime(t):
         if world == 1:
             return t
-        v = torch.tensor([t], dtype=torch.float64, device="cuda")
+        v = torch.tensor([t], dtype=torch.float64,
+                         device="cuda" if args.backend == "nccl" else "cpu")
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return float(v.item())
 
@@ -514,11 +526,13 @@ def main():
         "config": {"workload": f"{shape[0]}x{shape[1]}x{shape[2]} jittered grid (N={N}), "
                                f"{args.kernel.upper()} kernel amp=1 ls=2h noise={args.noise}+1e-6, "
                                f"k={k} lazy-greedy MI placements, dense-exact, one problem"
-                               + (f" candidate-sharded over {world} ranks (RCCL), Cholesky "
+                               + (f" candidate-sharded over {world} ranks "
+                                  f"({'RCCL' if args.backend == 'nccl' else args.backend}), Cholesky "
                                   "distributed (panel / SYRK shares all-gathered), inverse "
                                   "partitioned" if world > 1 else ""),
                    "N": N, "k": k, "parallelism": f"candidates{world}" if world > 1 else "single",
-                   "rccl_world_size": world if world > 1 else None},
+                   "rccl_world_size": world if world > 1 and args.backend == "nccl" else None,
+                   "backend": args.backend if world > 1 else None},
         "cholesky_gflops": chol_gflops,
         "cholesky_note": ("plain single-GPU potrf of the same Sigma" if world == 1 else
                           f"distributed potrf over {world} ranks (max-over-ranks time), "
