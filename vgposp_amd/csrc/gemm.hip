@@ -629,11 +629,13 @@ __global__ __launch_bounds__(256) void gemv_reduce_kernel(int64_t m, int nsplit,
   y[r * incy] = v;
 }
 
-// splits for the n == 1 paths: about 2048 waves in flight, >= 2048 (rows) / 256 (transposed)
-// K elements per split
+// splits for the n == 1 paths: about 8192 (rows) / 4096 (transposed) waves in flight, >= 1024
+// (rows) / 32 (transposed) K elements per split.  Short per-thread chains matter more than the
+// partials: the VGP step's M x M triangular L^-T x (m = 512, k <= 512) ran 41 us on 2 workgroups
+// of 256-long serial sums, its Kzb^T v (32,768 x 512) at 2.1 TB/s.
 static int gemv_splits(int64_t m, int64_t k, int transa) {
-  int64_t s = transa ? ceil_div(2048 * 64, std::max<int64_t>(m, 1)) : ceil_div(2048, m);
-  s = std::min<int64_t>(s, transa ? k / 256 : k / 2048);
+  int64_t s = transa ? ceil_div(4096 * 64, std::max<int64_t>(m, 1)) : ceil_div(8192, m);
+  s = std::min<int64_t>(s, transa ? k / 32 : k / 1024);
   return (int)std::max<int64_t>(std::min<int64_t>(s, 4096), 1);
 }
 
