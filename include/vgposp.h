@@ -333,6 +333,11 @@ int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, in
  *   threshold   |nom| or |denom| < threshold -> delta = 0 (:480: 1e-7; 1e-8 for alg. 2)
  *   cache_init  initial lazy-cache value (:690: INF = 1e8; +inf for alg. 2)
  * vgposp_greedy_init(...) == vgposp_greedy_init_ex(..., 0, 1e-8, +inf, ...).
+ * For n >= 8192 (and a stream not being captured) init synchronises the stream after the leading
+ * half of every recursion node of order >= 8192 and returns 0 as soon as `info` is set: a
+ * singular Sigma costs the factorization up to the failed pivot, not a whole factor + inverse,
+ * before the caller's jitter retry (placement_algorithm2.py:399-413's pinv has no failure mode).
+ * Sigma and the workspace are then undefined, as after any failed factorization.
  * vgposp_greedy_cache returns the device pointer of the lazy cache [n] (delta_cached): the
  * per-round snapshot delta_cached_iters[:, r] of the TF variant is a copy of it after round r. */
 int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int kmax, double jitter,

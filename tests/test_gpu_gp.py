@@ -167,3 +167,34 @@ def test_gprm_posterior_sampling_at_scale(mods):
     emp_mean = s.mean(0)
     sd = np.sqrt(np.diag(rc[0]) + gprm.jitter)
     assert np.all(np.abs(emp_mean - rm[0]) < 5 * sd / np.sqrt(4000) + 1e-9)
+
+
+def test_c1_sin_wave_eq_fit_8cube(mods):
+    """C1 as named: the RBF fit of 3D_sin_wave.py:126-209 on the 8 x 8 x 8 grid (main_GP_fit.py
+    shape).  Amplitude and length scale are assigned 0.5 through the softplus placeholders
+    (:190-197), the noise variance starts at softplus(INIT_OBSNOISEVAR), then Adam maximises
+    gp.log_prob (:181-183, :207-208).  The LML trajectory and the trained parameters equal the
+    oracle's fit_gp_adam over the same 512 points (rtol 1e-7)."""
+    _, _, gpf, _ = mods
+    from vgposp_amd.data_generation import grid_points, grid_observations
+    from vgposp_amd.psd_kernels import ExponentiatedQuadratic
+    X = grid_points((8, 8, 8), jitter=0.05, seed=2)
+    y = grid_observations(X, seed=3)
+    sess = gpf.reset_session()
+    amp, amp_assign, amp_p, lensc, lensc_assign, lensc_p, _, _, _, noise = \
+        gpf.tf_Placeholder_assign_test(np.array([1.0]), np.array([1.0]), 0.1)
+    _, a = sess.run([amp_assign, amp], feed_dict={amp_p: [0.5]})
+    _, l = sess.run([lensc_assign, lensc], feed_dict={lensc_p: [0.5]})
+    np.testing.assert_allclose([a[0], l[0]], [0.5, 0.5], rtol=1e-12)
+    gp = gpf.fit_gp(ExponentiatedQuadratic(amp, lensc), X, noise)
+    ll = gp.log_prob(y)
+    train_op = gpf.tf_train_gp_adam(ll, 0.05)
+    lls = gpf.tf_optimize_model_params(sess, 30, train_op, ll, None, None, None, None, None, y, None)
+    v0 = ogp.invert_softplus(0.5)
+    ref, theta = ogp.fit_gp_adam("eq", X, y, [v0], [v0], 0.1, 0.05, 30)
+    assert lls.shape == (31, 1)
+    np.testing.assert_allclose(lls, ref, rtol=1e-7)
+    assert lls[-1, 0] > lls[0, 0]  # the fit improves the likelihood
+    np.testing.assert_allclose(amp.numpy(), ogp.constrain(theta[:1]), rtol=1e-7)
+    np.testing.assert_allclose(lensc.numpy(), ogp.constrain(theta[1:2]), rtol=1e-7)
+    np.testing.assert_allclose(noise.numpy(), ogp.constrain(theta[2]), rtol=1e-7)

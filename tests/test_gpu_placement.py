@@ -117,6 +117,50 @@ def test_near_singular_cov_takes_jitter_path(seed):
         [int(a) for a in op.placement_algorithm_2(E, 6)]
 
 
+def test_singular_large_stops_early_and_matches(P):
+    """N = 16,384 with one location duplicated at column 9,000 (exactly equal rows, so Sigma is
+    singular).  (1) With that pivot pushed negative the factorization fails there and stops after
+    the leading half of the 8,192 node that holds it: no SYRK / trailing factor / inverse, so the
+    failed init costs well under a full one.  (2) On the singular Sigma the jitter path picks the
+    same sensors as the non-singular matrix without the duplicate (a duplicate's delta equals its
+    original's, the lower index wins the tie, and once either is placed the other's delta is 0)."""
+    import time
+    import torch
+    from vgposp_amd import linalg
+    from vgposp_amd.data_generation import grid_points, grid_spacing
+    shape = (32, 32, 16)
+    X = torch.as_tensor(grid_points(shape, jitter=0.05, seed=7), device="cuda")
+    n, src, dup, k = 16384, 1234, 9000, 6
+    Xd = torch.cat([X[:dup], X[src:src + 1], X[dup:n - 1]]).contiguous()  # Xd[dup] == Xd[src]
+    Sd = linalg.kernel_matrix("eq", Xd, None, 1.0, 2 * grid_spacing(shape), diag_shift=1e-2)[0]
+    Sd[dup, src] = Sd[src, dup] = Sd[src, src]  # row dup == row src: singular
+    keep = torch.cat([torch.arange(dup), torch.arange(dup + 1, n)]).cuda()
+    S = Sd[keep][:, keep].contiguous()  # the same locations without the duplicate
+
+    def timed_init(M):
+        g = P.GreedyPlacement(M, k, copy=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.init()
+        torch.cuda.synchronize()
+        return g, time.perf_counter() - t0
+
+    P.GreedyPlacement(S, k, copy=True).init()  # warm-up
+    Sneg = Sd.clone()
+    Sneg[dup, dup] -= 1e-3  # Schur complement -1e-3 at column dup
+    g, t_fail = timed_init(Sneg)
+    info = int(g.info.item())
+    assert info == dup + 1, info
+    h, t_full = timed_init(S)
+    assert int(h.info.item()) == 0
+    print(f"failed init {t_fail * 1e3:.1f} ms (info {info}), full init {t_full * 1e3:.1f} ms")
+    assert t_fail < 0.8 * t_full
+
+    ref = [int(a) for a in P.placement_algorithm_2(S, k)]
+    ref = [a if a < dup else a + 1 for a in ref]
+    assert [int(a) for a in P.placement_algorithm_2(Sd, k)] == ref
+
+
 @pytest.mark.parametrize("name", ["grid5", "grid654", "spd40", "grid8", "grid4"])
 def test_trace_matches_reference_print_lines(P, name, capsys):
     """The per-evaluation records (placement_algorithm2.py:205 'delta_y= .. y_st= ..' and :188

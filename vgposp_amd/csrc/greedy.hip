@@ -23,7 +23,7 @@
 namespace vgposp {
 
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
-              void* ws, hipStream_t stream);
+              void* ws, hipStream_t stream, bool early = false);
 size_t potrf_ws_bytes(int64_t n);
 int partial_inverse(double* A, int64_t n, int64_t lda, int64_t c0, int64_t c1, double* tmp,
                     void* ws, hipStream_t s);
@@ -471,8 +471,17 @@ extern "C" int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int 
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
                      n, lda, jitter, threshold, cache_init, w);
   VG_LAUNCH_CHECK();
-  int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_fact_ws(ws, w, n), s);
+  // early: a failed pivot (a singular cov_vv) ends the factorization where it is found, so the
+  // host's jitter retry does not pay for a whole O(n^3) factorization + inverse first
+  int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_fact_ws(ws, w, n), s,
+                     /*early=*/true);
   if (rc) return rc;
+  if (n >= 8192) {  // potrf_one already synchronised: skip the rest after a failed pivot
+    int h = 0;
+    VG_HIP(hipMemcpyAsync(&h, info, sizeof(int), hipMemcpyDeviceToHost, s));
+    VG_HIP(hipStreamSynchronize(s));
+    if (h != 0) return 0;
+  }
   // Q_ii = |M e_i|^2 -> part (reduced in the round-0 update)
   dim3 g((unsigned)ceil_div(n, TRMV_COLS), (unsigned)ceil_div(n, RC));
   const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);

@@ -335,6 +335,9 @@ struct Fact {
   int batch = 1;
   int64_t sA = 0, sW = 0;
   const double* ws0 = nullptr;
+  // stop early on a failed pivot: read `info` back after each large node's leading half (a
+  // stream sync per node of order >= EARLY_MIN) and abandon the rest of the factorization
+  bool early = false;
   double* leaf(int64_t col0) const { return linv_all + (col0 / NB) * NB * NB; }
   double* xblk(int64_t col0) const { return xinv + col0 * NBI; }
   int64_t stride(const void* p) const {
@@ -450,6 +453,19 @@ static int trtri_rec(const Fact& f, double* A, int64_t lda, int64_t n, int64_t c
   return pgemm(f, 0, 0, n2, n1, n2, -1.0, A22, lda, f.work, n1, 0.0, A21, lda, VGPOSP_FULL, 1, 0);
 }
 
+// Early stop (Fact::early): nodes of at least this order check `info` after their leading half.
+// A failed pivot at column j then costs about the factorization of the leading j columns plus
+// one node's panel, instead of the whole O(n^3) recursion and inverse.
+constexpr int64_t EARLY_MIN = 8192;
+constexpr int POTRF_STOPPED = 1;  // internal: info != 0, the rest of the recursion was skipped
+
+static int early_stop(const Fact& f) {
+  int h = 0;
+  VG_HIP(hipMemcpyAsync(&h, f.info, sizeof(int), hipMemcpyDeviceToHost, f.s));
+  VG_HIP(hipStreamSynchronize(f.s));
+  return h != 0 ? POTRF_STOPPED : 0;
+}
+
 // blocks: form the inverse of every NB < n <= NBI diagonal block (for trsm / trtri above it).
 static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0, bool blocks) {
   if (n <= NB) return leaf_factor(f, A, (int)n, col0, 0);
@@ -460,6 +476,7 @@ static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0, bool blo
   double* A22 = A21 + n1;
   const bool sub = blocks && !whole;  // inside a block the leaf-level path is used
   if ((rc = potrf_rec(f, A, n1, col0, sub))) return rc;
+  if (f.early && n >= EARLY_MIN && (rc = early_stop(f))) return rc;
   if ((rc = trsm_rec(f, A21, n2, f.lda, A, n1, col0, sub))) return rc;
   if ((rc = pgemm(f, 0, 1, n2, n2, n1, -1.0, A21, f.lda, A21, f.lda, 1.0, A22, f.lda,
                   VGPOSP_LOWER, 0, 0)))
@@ -526,12 +543,20 @@ int potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int batch, int 
 }
 
 int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, int* info,
-              void* ws, hipStream_t stream) {
+              void* ws, hipStream_t stream, bool early) {
   if (int rc = ensure_leaf_attr()) return rc;
   const bool blocks = n > NBI;
   Fact f = make_fact(n, lda, ws, diag_out, info, stream);
+  if (early && n >= EARLY_MIN) {
+    // a stream being captured into a graph cannot be synchronised: no early stop there
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) == hipSuccess) f.early = cs == hipStreamCaptureStatusNone;
+    else (void)hipGetLastError();  // status unknown: keep the fully asynchronous path
+  }
   int rc = potrf_rec(f, A, n, 0, blocks);
+  if (rc == POTRF_STOPPED) return 0;  // info holds the failed leading minor
   if (rc || !invert) return rc;
+  if (f.early && (rc = early_stop(f))) return rc == POTRF_STOPPED ? 0 : rc;
   return trtri_rec(f, A, lda, n, 0, blocks);
 }
 
@@ -785,7 +810,7 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
     return potrf_batched(A, n, lda, stride, batch, invert, diag_out, info, ws, s);
   for (int b = 0; b < batch; ++b) {
     int rc = potrf_one(A + b * stride, n, lda, invert, diag_out ? diag_out + (int64_t)b * n : nullptr,
-                       info + b, ws, s);
+                       info + b, ws, s, false);
     if (rc) return rc;
   }
   return 0;
