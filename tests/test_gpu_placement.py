@@ -145,15 +145,18 @@ def test_singular_large_stops_early_and_matches(P):
         torch.cuda.synchronize()
         return g, time.perf_counter() - t0
 
-    P.GreedyPlacement(S, k, copy=True).init()  # warm-up
-    Sneg = Sd.clone()
+    Sneg, Spos = Sd.clone(), Sd.clone()
     Sneg[dup, dup] -= 1e-3  # Schur complement -1e-3 at column dup
+    Spos[dup, dup] += 1e-3  # +1e-3: the same n and layout, positive definite
+    timed_init(Spos)  # warm-up
     g, t_fail = timed_init(Sneg)
     info = int(g.info.item())
     assert info == dup + 1, info
-    h, t_full = timed_init(S)
+    h, t_full = timed_init(Spos)
     assert int(h.info.item()) == 0
-    print(f"failed init {t_fail * 1e3:.1f} ms (info {info}), full init {t_full * 1e3:.1f} ms")
+    _, t_odd = timed_init(S)
+    print(f"failed init {t_fail * 1e3:.1f} ms (info {info}), full init {t_full * 1e3:.1f} ms, "
+          f"full init at the odd n = {n - 1}: {t_odd * 1e3:.1f} ms")
     assert t_fail < 0.8 * t_full
 
     ref = [int(a) for a in P.placement_algorithm_2(S, k)]
