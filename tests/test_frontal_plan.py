@@ -1,0 +1,69 @@
+"""CPU checks of the exact C4 path's host side: the nested-dissection plan
+(vgposp_amd.nested_dissection) and the batched multifrontal selected inversion it drives,
+restated in numpy (tests/numpy_frontal_backend.py) against a dense inverse."""
+import numpy as np
+import pytest
+
+from numpy_frontal_backend import selected_inverse_diag, tapered_entry_matrix
+from vgposp_amd.data_generation import grid_points, grid_spacing
+from vgposp_amd.local_placement import taper_support
+from vgposp_amd.nested_dissection import FrontalTree, stencil_radius
+
+
+@pytest.mark.parametrize("shape,beta,leaf", [
+    ((6, 7, 8), 4.0, 40),
+    ((5, 6, 7), 2.5, 30),
+    ((8, 8, 8), 4.0, 64),
+    ((3, 4, 20), 4.0, 10),
+    ((2, 2, 9), 4.0, 2),
+    ((4, 4, 4), 4.0, 512),     # a single leaf front
+])
+def test_selected_inverse_matches_dense(shape, beta, leaf):
+    offs, tau = taper_support(beta)
+    X = grid_points(shape, jitter=0.05, seed=1)
+    h = 2.0 * grid_spacing(shape)
+    C = tapered_entry_matrix(X, shape, offs, tau, lambda r2: np.exp(-0.5 * r2 / h ** 2),
+                             0.01 + 1e-6, 1e-6)
+    T = FrontalTree(shape, offs, leaf=leaf, pad=4)
+    d = selected_inverse_diag(T, C)
+    np.testing.assert_allclose(d, np.diag(np.linalg.inv(C)), rtol=1e-12)
+
+
+@pytest.mark.parametrize("shape,beta", [((16, 16, 16), 4.0), ((12, 9, 10), 2.5),
+                                        ((64, 32, 32), 4.0)])
+def test_plan_invariants(shape, beta):
+    offs, _ = taper_support(beta)
+    T = FrontalTree(shape, offs, leaf=512)
+    n = int(np.prod(shape))
+    assert T.r == max(stencil_radius(offs), 1)
+    # every node is a pivot of exactly one front, at its recorded position
+    seen = np.zeros(n, dtype=int)
+    for f in T.fronts:
+        seen[f.piv] += 1
+    assert np.all(seen == 1)
+    for g in T.groups:
+        assert g.p % 16 == 0 and g.u % 16 == 0
+        assert g.p >= g.p_max and g.u >= g.u_max
+        for s, fi in enumerate(g.fronts):
+            f = T.fronts[fi]
+            np.testing.assert_array_equal(g.piv[s, :len(f.piv)], f.piv)
+            assert np.all(g.piv[s, len(f.piv):] == -1)
+            assert np.all(np.diff(g.U[s, :g.ulen[s]]) > 0)
+            if f.parent >= 0:
+                # the parent-front positions of U are in range and distinct
+                pg = T.groups[g.parent_group[s]]
+                m = g.pmap[s, :g.ulen[s]]
+                assert np.all((m >= 0) & (m < pg.p + pg.u))
+                assert len(np.unique(m)) == len(m)
+    # groups are in a valid bottom-up order (children before parents)
+    for gi, g in enumerate(T.groups):
+        assert np.all((g.parent_group > gi) | (g.parent_group < 0))
+
+
+def test_plan_128cube_sizes():
+    """The C4 plan: 13 levels, the root separator is one 128 x 128 plane, ~8.7e13 flops."""
+    offs, _ = taper_support(4.0)
+    T = FrontalTree((128, 128, 128), offs, leaf=512)
+    assert len(T.groups) == 13
+    assert T.groups[-1].p == 128 * 128 and T.groups[-1].u == 0
+    assert 8e13 < T.flops(padded=False) < 9.5e13

@@ -527,14 +527,31 @@ static Fact make_fact(int64_t n, int64_t lda, void* ws, double* diag_out, int* i
 // leaves as one workgroup per matrix, the GEMMs with a batch grid dimension), so B small
 // factorizations cost the launches and the latency chain of one.  ws holds B copies of the
 // single-matrix workspace.
+// Per-matrix workspace of a batched factorization without the split-K partials (large batches
+// fill the GPU through the batch dimension; 16 MB of partials per matrix would not fit).
+size_t potrf_ws_bytes_opt(int64_t n, bool use_part) {
+  return potrf_ws_bytes(n) - ((!use_part && n > NB) ? (size_t)PART_ELEMS * sizeof(double) : 0);
+}
+
 int potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int batch, int invert,
-                  double* diag_out, int* info, void* ws, hipStream_t stream) {
+                  double* diag_out, int* info, void* ws, hipStream_t stream, bool use_part) {
   if (int rc = ensure_leaf_attr()) return rc;
+  if (n <= NB) {
+    // one launch, one workgroup per matrix (no workspace needed)
+    ProfScope ps("potrf_diag", stream, batch * 2.0 * n * (double)n * n / 3.0,
+                 batch * 16.0 * n * (double)n);
+    hipLaunchKernelGGL(potrf_leaf_kernel, dim3(batch), dim3(LEAF_THREADS), leaf_shmem(), stream, A,
+                       lda, (int)n, (int64_t)0, invert, (double*)nullptr, diag_out, info, sA,
+                       (int64_t)0, batch > 1 ? n : (int64_t)-1);
+    VG_LAUNCH_CHECK();
+    return 0;
+  }
   const bool blocks = n > NBI;
   Fact f = make_fact(n, lda, ws, diag_out, info, stream);
+  if (!use_part) f.part = nullptr;
   f.batch = batch;
   f.sA = sA;
-  f.sW = (int64_t)(potrf_ws_bytes(n) / sizeof(double));
+  f.sW = (int64_t)(potrf_ws_bytes_opt(n, use_part) / sizeof(double));
   f.ws0 = static_cast<const double*>(ws);
   f.diag_n = n;
   int rc = potrf_rec(f, A, n, 0, blocks);
@@ -807,7 +824,7 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
     return 0;
   }
   if (batch > 1 && ws_bytes >= (size_t)batch * potrf_ws_bytes(n))
-    return potrf_batched(A, n, lda, stride, batch, invert, diag_out, info, ws, s);
+    return potrf_batched(A, n, lda, stride, batch, invert, diag_out, info, ws, s, true);
   for (int b = 0; b < batch; ++b) {
     int rc = potrf_one(A + b * stride, n, lda, invert, diag_out ? diag_out + (int64_t)b * n : nullptr,
                        info + b, ws, s, false);
