@@ -53,8 +53,8 @@ def parse():
     p.add_argument("--no-vgp", action="store_true", help="skip the C3 / C5 VGP training lines")
     p.add_argument("--no-c2", action="store_true", help="skip the C2 assembly + potrf line")
     p.add_argument("--vgp-steps", type=int, default=10)
-    p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 local greedy) line")
-    p.add_argument("--c4-steps", type=int, default=10)
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 exact algorithm 3) line")
+    p.add_argument("--c4-steps", type=int, default=3)
     p.add_argument("--no-splits", action="store_true",
                    help="skip the N > 1 independent-splits extra")
     p.add_argument("--backend", default="nccl",
@@ -253,48 +253,74 @@ def c2_line(reps=5):
 
 
 def c4_line(args, world, rank, barrier, maxtime):
-    """Config C4: 128^3 = 2,097,152 candidates, k = 50, the local-kernel greedy
-    (algorithm 3 with epsilon-local deltas on the beta = 4 taper, window cutoff 3), candidates
-    sharded over the ranks by i0-planes with one 16-byte key all-gather per pick."""
+    """Config C4: 128^3 = 2,097,152 candidates, k = 50, the reference's algorithm 3
+    (snippets_a3.py:43-364) on the beta = 4 tapered covariance, window cutoff 3 — exact: the
+    denominators over V \\ (A u {y}) from a nested-dissection multifrontal selected inverse
+    (fp64 MFMA fronts) plus one CG column per pick (vgposp_amd.sparse_placement).  One step = the
+    selected inverse + all k rounds (the symbolic plan depends only on the grid shape and the taper
+    support and is built once, outside the timed region, like an FFT plan; plan_s reports it)."""
     import torch
 
     from vgposp_amd import _lib
-    from vgposp_amd.local_placement import HipLocalBackend, LocalGreedyPlacement, plane_slabs
+    from vgposp_amd.sparse_placement import ExactTaperPlacement
     from vgposp_amd.workloads import c4_grid
     X, shape, ls = c4_grid()
-    c0, c1 = plane_slabs(shape, world)[rank]
     k, beta, cutoff = args.k, 4.0, 3
-    b = HipLocalBackend(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6, c0=c0,
-                        c1=c1)
-    g = LocalGreedyPlacement(b)
-    for _ in range(2):
-        g.run(k)
+    run = ExactTaperPlacement(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6)
+    run.run()
+    torch.cuda.synchronize()
+    run.check()
+    ref = run.greedy.picks[:k].clone()
     reps = args.c4_steps
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        g.run(k)
+        run.run()
     torch.cuda.synchronize()
     barrier()
     dt = maxtime(time.perf_counter() - t0) / reps
-    b.check()
+    run.check()
+    same = bool(torch.equal(ref, run.greedy.picks[:k]))
     _lib.prof_enable(True)
-    g.run(k)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    run.sel.run(out=run.qdiag)
+    ev[1].record()
+    run.greedy.run(run.qdiag, k)
+    ev[2].record()
+    torch.cuda.synchronize()
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
-    out = {"metric": "greedy sensor placements/sec", "value": k / dt, "unit": "placements/s",
-           "ms_per_step": dt * 1e3, "n_gpus": world, "scaling": "strong",
-           "config": {"workload": "C4: 128^3 jittered grid (N=2,097,152), EQ amp 1 ls 2h, "
-                                  f"noise {args.noise}+1e-6, beta-decay taper beta={beta} "
-                                  f"(support {b.m} points), window cutoff {cutoff}, k={k}, "
-                                  "local-kernel algorithm 3",
-                      "N": int(np.prod(shape)), "k": k, "parallelism": f"candidates{world}"},
-           "picks_head": [int(v) for v in b.picks[:6].cpu()],
-           "breakdown_ms": {n: v[0] for n, v in prof.items()},
-           "note": ("latency-bound: per pick an arg-max, a 216-candidate window re-score and (N > 1) "
-                    "one key all-gather; round 0 scores every candidate once")}
-    return out
+    sel_ms, rounds_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    fl_alg = run.sel.tree.flops(padded=False)
+    fl_pad = run.sel.flops()
+    gms, gl, gfl, _ = prof.get("gemm_f64", (0.0, 0, 0.0, 0.0))
+    gemm_tf = gfl / (gms * 1e-3) / 1e12 if gms else None
+    return {"metric": "greedy sensor placements/sec", "value": k / dt, "unit": "placements/s",
+            "ms_per_step": dt * 1e3, "n_gpus": world, "scaling": "replicas" if world > 1 else None,
+            "config": {"workload": "C4: 128^3 jittered grid (N=2,097,152), EQ amp 1 ls 2h, "
+                                   f"noise {args.noise}+1e-6, beta-decay taper beta={beta} "
+                                   f"(support {run.prob.m} points), window cutoff {cutoff}, k={k}, "
+                                   "exact algorithm 3 (dense-equivalent deltas, TF constants)",
+                       "N": int(np.prod(shape)), "k": k,
+                       "parallelism": "single" if world == 1 else f"replicated x{world}"},
+            "picks_head": [int(v) for v in ref[:6].cpu()],
+            "deterministic_selection": same,
+            "selected_inverse": {
+                "ms": sel_ms, "flops_algorithmic": fl_alg, "flops_padded": fl_pad,
+                "tflops_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12,
+                "mfma_frac_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                "gemm_tflops": gemm_tf,
+                "gemm_frac": gemm_tf / FP64_MFMA_PEAK_TFLOPS if gemm_tf else None,
+                "gemm_ms": gms, "gemm_launches": gl,
+                "fronts": len(run.sel.tree.fronts), "levels": len(run.sel.tree.groups),
+                "plan_s": run.sel.plan_s},
+            "rounds_ms": rounds_ms, "cg_iterations_per_pick": run.greedy.cg_iters,
+            "breakdown_ms": {n: v[0] for n, v in prof.items()},
+            "note": ("selected inverse = nested-dissection multifrontal Cholesky + Takahashi "
+                     "recurrences on batched fp64 MFMA fronts; per pick one CG column Q e_a and a "
+                     "216-candidate window re-score with |A| x |A| solves")}
 
 
 def splits_line(args, world, barrier, maxtime, rank):

@@ -472,14 +472,16 @@ int vgposp_local_run(VGPOSP_LOCAL_ARGS, int k, int64_t* picks, double* pick_delt
  *     front eliminating each node and its pivot position; piv [nf][p] (-1 = padding: identity);
  *     U [nf][u] ascending, ulen [nf]; order [nf]: the fronts' post-order ids.
  *   vgposp_front_extend_add: parent front += the lower triangle of each child's update UUc
- *     ([nfc][uc][uc]) at positions pmap [nfc][uc] (-1 = padding) of front pslot[c] of the parent
- *     group (PP / UP / UU, p, u); only children with sibling[c] == sib (call once per sibling
- *     index: siblings share a parent).
+ *     ([nfc][uc][uc]) at positions pmap [nfc][uc] (-1 = padding) of its parent front, which sits
+ *     at element offsets par_off [nfc][3] of the parent level's PP / UP / UU buffers with padded
+ *     sizes par_dim [nfc][2] = (p, u); only children with sibling[c] == sib (call once per
+ *     sibling index: siblings share a parent).
  *   vgposp_front_factor:     per front, PP <- M = L^-1 (F_PP = L L^T), UU -= L_UP L_UP^T with
  *     L_UP = F_UP M^T, UP <- W = L_UP M.  info [nf] (potrf convention).  ws:
  *     vgposp_front_factor_workspace_bytes(p, u, nf).
- *   vgposp_front_gather:     child's full Q_UU [nfc][uc][uc] <- the parent group's Q front
- *     (QPP lower, QUP, QUU full) at (pmap[a], pmap[b]); 0 on padding.
+ *   vgposp_front_gather:     child's full Q_UU [nfc][uc][uc] <- its parent's Q front (QPP lower,
+ *     QUP, QUU full; the parent level's buffers, par_off / par_dim as above) at
+ *     (pmap[a], pmap[b]); 0 on padding.
  *   vgposp_front_selinv:     QPP <- M^T M - W^T T (lower), QUP <- T = -QUU W (out of place).
  *   vgposp_front_diag:       out[piv[f][k]] <- QPP[f][k][k] for piv >= 0.
  * --------------------------------------------------------------------------------------------- */
@@ -491,13 +493,13 @@ int vgposp_front_assemble(int kind, const double* X, int64_t I0, int64_t I1, int
                           const int* U, int64_t u, const int* ulen, const int* order, int nf,
                           double* PP, double* UP, void* stream);
 int vgposp_front_extend_add(const double* UUc, int64_t uc, int nfc, const int* pmap,
-                            const int* pslot, const int* sibling, int sib, double* PP, double* UP,
-                            double* UU, int64_t p, int64_t u, void* stream);
+                            const int64_t* par_off, const int* par_dim, const int* sibling, int sib,
+                            double* PP, double* UP, double* UU, void* stream);
 int vgposp_front_factor(double* PP, double* UP, double* UU, int64_t p, int64_t u, int nf,
                         int* info, void* ws, size_t ws_bytes, void* stream);
-int vgposp_front_gather(const double* QPP, const double* QUP, const double* QUU, int64_t p,
-                        int64_t u, const int* pmap, const int* pslot, int nfc, int64_t uc,
-                        double* QUUc, void* stream);
+int vgposp_front_gather(const double* QPP, const double* QUP, const double* QUU,
+                        const int* pmap, const int64_t* par_off, const int* par_dim, int nfc,
+                        int64_t uc, double* QUUc, void* stream);
 int vgposp_front_selinv(const double* M, const double* W, const double* QUU, int64_t p, int64_t u,
                         int nf, double* QPP, double* QUP, void* stream);
 int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, double* out,
@@ -505,30 +507,36 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
 
 /* The rounds of exact algorithm 3 on the tapered covariance (taper arguments as above; kmax <= 128;
  * cutoff: the window [i_d - cutoff, i_d + cutoff) of snippets_a3.py:190-303; threshold: |nom| or
- * |denom| below -> delta 0, snippets_a2.py:480).  qdiag [N]: diag((Sigma + jitter I)^-1) from the
- * front_* calls; cache [N] f64 (delta_cached), selected [N] uint8, both caller-owned.
+ * |denom| below -> delta 0, snippets_a2.py:480; radius: the stencil radius (largest offset
+ * component); cg_iters: conjugate-gradient iterations per column).  qdiag [N]:
+ * diag((Sigma + jitter I)^-1) from the front_* calls; cache [N] f64 (delta_cached), selected [N]
+ * uint8, both caller-owned.
  *   vgposp_exact_prepare: the stencil coefficients, round 0 (every candidate: nom = s_yy,
  *     denom = 1 / Q_yy - jitter) and the arg-max keys; clears `selected`.
  *   vgposp_exact_round:   pick `round` = the arg-max of the cache over V \ A (lowest index on ties),
- *     picks[round] / pick_delta[round]; unless `last`: q = Q e_pick by `cg_iters` conjugate-gradient
- *     iterations on Sigma + jitter I (stopping early once |r| <= cg_tol), the next rows of
- *     chol(Q_AA) and chol(Sigma_AA + jitter I), and the window re-score
+ *     picks[round] / pick_delta[round]; unless `last`: q = Q e_pick by cg_iters CG iterations on
+ *     Sigma + jitter I (stopping early once |r| <= cg_tol) on the box of half-width
+ *     radius * cg_iters around the pick (the Krylov vectors are exactly zero beyond it), the next
+ *     rows of chol(Q_AA) and chol(Sigma_AA + jitter I), and the window re-score
  *       nom = s_yy - |LS^-1 s_Ay|^2,  denom = 1 / (Q_yy - |LQ^-1 q_Ay|^2) - jitter.
- *   vgposp_exact_buffers: device addresses of the Q columns [kmax][N] and the CG state (int [2]:
- *     converged flag, iterations of the last solve). */
-size_t vgposp_exact_workspace_bytes(int64_t n, int m, int kmax);
+ *   vgposp_exact_buffers: device addresses of the columns [kmax][b0 b1 b2] (box-local, C order,
+ *     box dims b_d = min(2 radius cg_iters + 1, I_d)), their box origins int64 [kmax][3] and the
+ *     CG state (int [2]: converged flag, iterations of the last solve). */
+size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
+                                    int cg_iters);
 int vgposp_exact_prepare(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2, double amp,
                          double ls, double diag_shift, double jitter, double threshold,
                          const int* offsets, int m, const double* tau, int ntau, int kmax,
-                         int cutoff, const double* qdiag, double* cache, uint8_t* selected,
-                         void* ws, size_t ws_bytes, void* stream);
+                         int cutoff, int radius, int cg_iters, const double* qdiag, double* cache,
+                         uint8_t* selected, void* ws, size_t ws_bytes, void* stream);
 int vgposp_exact_round(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2, double amp,
                        double ls, double diag_shift, double jitter, double threshold,
                        const int* offsets, int m, const double* tau, int ntau, int kmax,
-                       int cutoff, const double* qdiag, double* cache, uint8_t* selected, void* ws,
-                       size_t ws_bytes, int round, int last, int64_t* picks, double* pick_delta,
-                       int cg_iters, double cg_tol, void* stream);
-int vgposp_exact_buffers(void* ws, int64_t n, int m, int kmax, double** qcols, int** cgstate);
+                       int cutoff, int radius, int cg_iters, const double* qdiag, double* cache,
+                       uint8_t* selected, void* ws, size_t ws_bytes, int round, int last,
+                       int64_t* picks, double* pick_delta, double cg_tol, void* stream);
+int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
+                         int cg_iters, double** qcols, int64_t** boxlo, int** cgstate);
 
 /* ---------------------------------------------------------------------------------------------
  * TF1 AdamOptimizer step on a device parameter vector (tf.train.AdamOptimizer in

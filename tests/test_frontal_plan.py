@@ -61,9 +61,19 @@ def test_plan_invariants(shape, beta):
 
 
 def test_plan_128cube_sizes():
-    """The C4 plan: 13 levels, the root separator is one 128 x 128 plane, ~8.7e13 flops."""
+    """The C4 plan: 13 levels, the root separator is one 128 x 128 plane, ~8.7e13 flops, and the
+    size-bucketed groups pad away less than 3 % of them."""
     offs, _ = taper_support(4.0)
     T = FrontalTree((128, 128, 128), offs, leaf=512)
-    assert len(T.groups) == 13
+    assert len(T.levels) == 13
     assert T.groups[-1].p == 128 * 128 and T.groups[-1].u == 0
     assert 8e13 < T.flops(padded=False) < 9.5e13
+    assert T.flops(padded=True) < 1.03 * T.flops(padded=False)
+    # level offsets tile each level's buffers exactly
+    for lvl in T.levels:
+        end = [0, 0, 0]
+        for gi in lvl["groups"]:
+            g = T.groups[gi]
+            assert list(g.off) == end
+            end = [end[0] + g.nf * g.p * g.p, end[1] + g.nf * g.u * g.p, end[2] + g.nf * g.u * g.u]
+        assert end == lvl["size"]

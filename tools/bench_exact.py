@@ -43,6 +43,17 @@ def main():
         wall = time.perf_counter() - t0
         r = (wall, ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]))
         best = r if best is None or r[0] < best[0] else best
+    evs = []
+
+    def tick(tag):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        evs.append((tag, e))
+    run.sel.run(out=run.qdiag, timer=tick)
+    torch.cuda.synchronize()
+    phases = {}
+    for (t0_, e0), (t1_, e1) in zip(evs[:-1], evs[1:]):
+        phases[f"{t1_[0]}{run.sel.tree.levels[t1_[1]]['depth']}"] = round(e0.elapsed_time(e1), 3)
     _lib.prof_enable(True)
     run.sel.run(out=run.qdiag)
     run.greedy.run(run.qdiag, k)
@@ -60,7 +71,7 @@ def main():
            "cg_iters": run.greedy.cg_iters, "cg_used_last": run.greedy.cg_iterations_used(),
            "picks_head": [int(v) for v in picks[:8].cpu()],
            "prof": {kname: [round(v[0], 3), v[1]] for kname, v in prof.items()},
-           "groups": run.sel.tree.summary()}
+           "phases_ms": phases, "groups": run.sel.tree.summary()}
     print(json.dumps(out), flush=True)
 
 

@@ -54,7 +54,8 @@ _LOCAL = [_i32, _c_void_p, _i64, _i64, _i64, _f64, _f64, _f64, _f64, _f64, _c_vo
 
 # the common leading arguments of vgposp_exact_prepare / vgposp_exact_round
 _EXACT = [_i32, _c_void_p, _i64, _i64, _i64, _f64, _f64, _f64, _f64, _f64, _c_void_p, _i32,
-          _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size]
+          _c_void_p, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+          _size]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -132,20 +133,20 @@ SIGNATURES = {
                                      _c_void_p, _i64, _c_void_p, _i64, _c_void_p, _c_void_p, _i32,
                                      _c_void_p, _c_void_p, _c_void_p]),
     "vgposp_front_extend_add": (_i32, [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
-                                       _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i64,
+                                       _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
                                        _c_void_p]),
     "vgposp_front_factor": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i32, _c_void_p,
                                    _c_void_p, _size, _c_void_p]),
-    "vgposp_front_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
+    "vgposp_front_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                    _c_void_p, _i32, _i64, _c_void_p, _c_void_p]),
     "vgposp_front_selinv": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i32, _c_void_p,
                                    _c_void_p, _c_void_p]),
     "vgposp_front_diag": (_i32, [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p]),
-    "vgposp_exact_workspace_bytes": (_size, [_i64, _i32, _i32]),
+    "vgposp_exact_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32, _i32, _i32]),
     "vgposp_exact_prepare": (_i32, _EXACT + [_c_void_p]),
-    "vgposp_exact_round": (_i32, _EXACT + [_i32, _i32, _c_void_p, _c_void_p, _i32, _f64,
-                                           _c_void_p]),
-    "vgposp_exact_buffers": (_i32, [_c_void_p, _i64, _i32, _i32, ctypes.POINTER(_c_void_p),
+    "vgposp_exact_round": (_i32, _EXACT + [_i32, _i32, _c_void_p, _c_void_p, _f64, _c_void_p]),
+    "vgposp_exact_buffers": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
+                                    ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
                                     ctypes.POINTER(_c_void_p)]),
     "vgposp_adam_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64, _f64,
                                   _f64, _f64, _c_void_p, _f64, _c_void_p]),

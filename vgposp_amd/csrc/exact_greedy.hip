@@ -39,17 +39,22 @@ struct ExactWS {
   long long* bidx;
   double* sval;       // [nsb]
   long long* sidx;
-  double* r;          // CG residual [n]
-  double* p0;         // CG directions [n] x 2
+  // CG on the box of half-width H around the pick (clipped into the grid): the Krylov vectors of
+  // a solve of S e_a are exactly zero beyond H = iterations x stencil radius, so the box holds
+  // every non-zero of the full-grid iteration.  Box-local vectors, [bv] each.
+  double* r;          // residual
+  double* p0;         // directions (two, alternating)
   double* p1;
-  double* q;          // A p [n]
+  double* q;          // A p
+  long long* boxlo;   // [kmax][3] box origin of each pick's column
+  long long b0, b1, b2, H;
   double* part_pq;    // [CG_BLOCKS]
   double* part_rr;    // [CG_BLOCKS]
   double* rr;         // [maxit + 2] residual norms per iteration
   int* cgstate;       // [4]: done flag, iterations of the last solve
   double* LS;         // [kmax][kmax] chol(S_AA + eps I)
   double* LQ;         // [kmax][kmax] chol(Q_AA)
-  double* Qcols;      // [kmax][n]
+  double* Qcols;      // [kmax][bv]: Q e_{a_t} on pick t's box (zero outside it)
   size_t bytes;
 };
 
@@ -57,8 +62,15 @@ constexpr int CG_MAXIT = 512;
 
 static size_t ealign(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static ExactWS exact_layout(void* base, int64_t n, int m, int kmax) {
+static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
+                            int64_t H) {
   ExactWS w{};
+  const int64_t n = I0 * I1 * I2;
+  w.H = H;
+  w.b0 = std::min<int64_t>(2 * H + 1, I0);
+  w.b1 = std::min<int64_t>(2 * H + 1, I1);
+  w.b2 = std::min<int64_t>(2 * H + 1, I2);
+  const int64_t bv = w.b0 * w.b1 * w.b2;
   const int64_t nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
   char* p = static_cast<char*>(base);
   size_t off = 0;
@@ -72,17 +84,18 @@ static ExactWS exact_layout(void* base, int64_t n, int m, int kmax) {
   w.bidx = (long long*)take(8 * nblk);
   w.sval = (double*)take(8 * nsb);
   w.sidx = (long long*)take(8 * nsb);
-  w.r = (double*)take(8 * (size_t)n);
-  w.p0 = (double*)take(8 * (size_t)n);
-  w.p1 = (double*)take(8 * (size_t)n);
-  w.q = (double*)take(8 * (size_t)n);
+  w.r = (double*)take(8 * (size_t)bv);
+  w.p0 = (double*)take(8 * (size_t)bv);
+  w.p1 = (double*)take(8 * (size_t)bv);
+  w.q = (double*)take(8 * (size_t)bv);
+  w.boxlo = (long long*)take(8 * 3 * (size_t)kmax);
   w.part_pq = (double*)take(8 * CG_BLOCKS);
   w.part_rr = (double*)take(8 * CG_BLOCKS);
   w.rr = (double*)take(8 * (CG_MAXIT + 2));
   w.cgstate = (int*)take(16);
   w.LS = (double*)take(8 * (size_t)kmax * kmax);
   w.LQ = (double*)take(8 * (size_t)kmax * kmax);
-  w.Qcols = (double*)take(8 * (size_t)kmax * n);
+  w.Qcols = (double*)take(8 * (size_t)kmax * bv);
   w.bytes = off;
   return w;
 }
@@ -118,6 +131,15 @@ __device__ __forceinline__ double sigma_off(const EArgs& a, long long i, long lo
   const double d0 = a.X[3 * i] - a.X[3 * j], d1 = a.X[3 * i + 1] - a.X[3 * j + 1],
                d2 = a.X[3 * i + 2] - a.X[3 * j + 2];
   return t * kfun<KIND>(d0 * d0 + d1 * d1 + d2 * d2, a.tla, a.inv_ls, a.inv_ls2);
+}
+
+// Q e_{a_r} at grid node y: its box value, 0 outside the box.
+__device__ __forceinline__ double qcol_at(const ExactWS& w, int r, long long y, long long I1,
+                                          long long I2) {
+  const long long* lo = w.boxlo + 3 * r;
+  const long long l0 = y / (I1 * I2) - lo[0], l1 = (y / I2) % I1 - lo[1], l2 = y % I2 - lo[2];
+  if (l0 < 0 || l0 >= w.b0 || l1 < 0 || l1 >= w.b1 || l2 < 0 || l2 >= w.b2) return 0.0;
+  return w.Qcols[(size_t)r * (w.b0 * w.b1 * w.b2) + (l0 * w.b1 + l1) * w.b2 + l2];
 }
 
 __device__ __forceinline__ double delta_of(double nom, double den, double thr) {
@@ -216,8 +238,9 @@ __global__ __launch_bounds__(256) void exact_super_keys_kernel(const double* bva
 // (placement_algorithm2.py:24-50 via sparse_argmax_cache_linear); A <- A u {y*}, the cache entry of
 // y* <- 0 (snippets_a3.py:162-168), its block keys refreshed; CG set up for q = Q e_{y*}.
 __global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
-    double* cache, unsigned char* sel, long long n, ExactWS w, long long nblk, long long nsb,
-    int round, long long* picks, double* pick_delta, double* x) {
+    double* cache, unsigned char* sel, long long I0, long long I1, long long I2, ExactWS w,
+    long long nblk, long long nsb, int round, long long* picks, double* pick_delta, int solve) {
+  const long long n = I0 * I1 * I2;
   __shared__ double sv[SEL_THREADS / 64];
   __shared__ long long si[SEL_THREADS / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -246,9 +269,16 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
       if (idx >= 0) {
         sel[idx] = 1;
         cache[idx] = 0.0;
-        if (x) {
-          w.r[idx] = 1.0;
-          w.p0[idx] = 1.0;
+        if (solve) {
+          // the column's box: [a - H, a + H] per axis, shifted inside the grid
+          const long long a0 = idx / (I1 * I2), a1 = (idx / I2) % I1, a2 = idx % I2;
+          const long long lo0 = min(max(a0 - w.H, 0LL), I0 - w.b0);
+          const long long lo1 = min(max(a1 - w.H, 0LL), I1 - w.b1);
+          const long long lo2 = min(max(a2 - w.H, 0LL), I2 - w.b2);
+          w.boxlo[3 * round] = lo0;
+          w.boxlo[3 * round + 1] = lo1;
+          w.boxlo[3 * round + 2] = lo2;
+          w.r[((a0 - lo0) * w.b1 + (a1 - lo1)) * w.b2 + (a2 - lo2)] = 1.0;
         }
       }
       w.rr[0] = 1.0;
@@ -293,12 +323,34 @@ __device__ __forceinline__ void block_partial(double v, double* part, double* re
   }
 }
 
+// Box-local node l -> (grid coordinates, inside the active region of iteration it).  The
+// iterate's support after `it` steps lies within `it` stencil radii of the pick in every axis; the
+// kernels skip the rest of the box (its entries are and stay exactly zero).
+struct BoxNode {
+  long long g0, g1, g2;
+  bool active;
+};
+
+__device__ __forceinline__ BoxNode box_node(const ExactWS& w, long long l, const long long* lo,
+                                            long long a0, long long a1, long long a2,
+                                            long long rad) {
+  BoxNode b;
+  const long long l0 = l / (w.b1 * w.b2), l1 = (l / w.b2) % w.b1, l2 = l % w.b2;
+  b.g0 = lo[0] + l0;
+  b.g1 = lo[1] + l1;
+  b.g2 = lo[2] + l2;
+  b.active = llabs(b.g0 - a0) <= rad && llabs(b.g1 - a1) <= rad && llabs(b.g2 - a2) <= rad;
+  return b;
+}
+
 // CG iteration it, part A: beta from the last residual norms, p_it = r + beta p_{it-1} (computed
 // for the neighbours on the fly, written for this thread's own nodes), q = (S + eps I) p_it and
 // the partials of p_it . q.  Converged (|r|^2 <= tol2) -> every block returns; block 0 records it.
 __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I0, long long I1,
                                                           long long I2, const int* offs, int m1,
-                                                          int it, double tol2) {
+                                                          int srad, int round,
+                                                          const long long* picks, int it,
+                                                          double tol2) {
   __shared__ double red[CG_T / 64];
   if (w.cgstate[0]) return;
   const double rr = w.rr[it];
@@ -312,41 +364,57 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   const double beta = it == 0 ? 0.0 : rr / w.rr[it - 1];
   const double* pold = (it & 1) ? w.p0 : w.p1;  // p_{it-1}
   double* pnew = (it & 1) ? w.p1 : w.p0;        // p_it
-  const long long n = I0 * I1 * I2;
+  const long long a = picks[round];
+  const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
+  const long long* lo = w.boxlo + 3 * round;
+  const long long bv = w.b0 * w.b1 * w.b2;
+  const long long rad = min((long long)(it + 1) * srad, w.H);
   const int m = m1 + 1;
   double acc = 0.0;
-  for (long long i = (long long)blockIdx.x * CG_T + threadIdx.x; i < n; i += (long long)CG_BLOCKS * CG_T) {
-    const double pi = it == 0 ? w.r[i] : fma(beta, pold[i], w.r[i]);
-    const double* c = w.coef + i * m;
+  for (long long l = (long long)blockIdx.x * CG_T + threadIdx.x; l < bv; l += (long long)CG_BLOCKS * CG_T) {
+    const BoxNode nd = box_node(w, l, lo, a0, a1, a2, rad);
+    if (!nd.active) continue;
+    const double pi = it == 0 ? w.r[l] : fma(beta, pold[l], w.r[l]);
+    const double* c = w.coef + ((nd.g0 * I1 + nd.g1) * I2 + nd.g2) * m;
     double s = c[0] * pi;
-    const long long i0 = i / (I1 * I2), i1 = (i / I2) % I1, i2 = i % I2;
     for (int o = 0; o < m1; ++o) {
       const double cv = c[1 + o];
-      if (cv == 0.0) continue;
-      const long long j = ((i0 + offs[3 * o]) * I1 + (i1 + offs[3 * o + 1])) * I2 + i2 + offs[3 * o + 2];
+      if (cv == 0.0) continue;  // outside the grid
+      const long long j0 = nd.g0 + offs[3 * o] - lo[0], j1 = nd.g1 + offs[3 * o + 1] - lo[1],
+                      j2 = nd.g2 + offs[3 * o + 2] - lo[2];
+      if (j0 < 0 || j0 >= w.b0 || j1 < 0 || j1 >= w.b1 || j2 < 0 || j2 >= w.b2) continue;
+      const long long j = (j0 * w.b1 + j1) * w.b2 + j2;
       const double pj = it == 0 ? w.r[j] : fma(beta, pold[j], w.r[j]);
       s = fma(cv, pj, s);
     }
-    pnew[i] = pi;
-    w.q[i] = s;
+    pnew[l] = pi;
+    w.q[l] = s;
     acc = fma(pi, s, acc);
   }
   block_partial(acc, w.part_pq, red);
 }
 
 // CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2.
-__global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long n, int it,
+__global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I1, long long I2,
+                                                          int srad, int round,
+                                                          const long long* picks, int it,
                                                           double* __restrict__ x) {
   __shared__ double red[CG_T / 64];
   if (w.cgstate[0]) return;
   const double pq = sum_partials(w.part_pq, red);
   const double alpha = w.rr[it] / pq;
   const double* p = (it & 1) ? w.p1 : w.p0;
+  const long long a = picks[round];
+  const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
+  const long long* lo = w.boxlo + 3 * round;
+  const long long bv = w.b0 * w.b1 * w.b2;
+  const long long rad = min((long long)(it + 1) * srad, w.H);
   double acc = 0.0;
-  for (long long i = (long long)blockIdx.x * CG_T + threadIdx.x; i < n; i += (long long)CG_BLOCKS * CG_T) {
-    x[i] = fma(alpha, p[i], x[i]);
-    const double ri = fma(-alpha, w.q[i], w.r[i]);
-    w.r[i] = ri;
+  for (long long l = (long long)blockIdx.x * CG_T + threadIdx.x; l < bv; l += (long long)CG_BLOCKS * CG_T) {
+    if (!box_node(w, l, lo, a0, a1, a2, rad).active) continue;
+    x[l] = fma(alpha, p[l], x[l]);
+    const double ri = fma(-alpha, w.q[l], w.r[l]);
+    w.r[l] = ri;
     acc = fma(ri, ri, acc);
   }
   block_partial(acc, w.part_rr, red);
@@ -374,7 +442,6 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_update_kernel(
   const int km = a.kmax;
   const long long at = picks[round];
   if (at < 0) return;
-  const double* qt = w.Qcols + (size_t)round * a.n;
   // row `round` of the two factors, one wave each, built in LDS
   if (wave < 2) {
     const double* L = wave == 0 ? w.LQ : w.LS;
@@ -382,7 +449,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_update_kernel(
     for (int r = 0; r <= round; ++r) {
       const long long ar = picks[r];
       double v;
-      if (wave == 0) v = qt[ar];
+      if (wave == 0) v = qcol_at(w, round, ar, a.I1, a.I2);
       else v = (r == round) ? sigma_diag<KIND>(a) + a.jitter : sigma_off<KIND>(a, at, ar);
       double acc = 0.0;
       // off-diagonal: row . L[r][:r];  diagonal (r == round): |row[:r]|^2
@@ -423,7 +490,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_update_kernel(
     for (int r = 0; r <= round; ++r) {
       const long long ar = picks[r];
       double vs = sigma_off<KIND>(a, ar, y);
-      double vq = w.Qcols[(size_t)r * a.n + y];
+      double vq = qcol_at(w, r, y, a.I1, a.I2);
       const double* ls = r == round ? rowbuf[1] : w.LS + (size_t)r * km;
       const double* lq = r == round ? rowbuf[0] : w.LQ + (size_t)r * km;
       for (int s = 0; s < r; ++s) {
@@ -476,10 +543,12 @@ namespace {
   VG_CHECK_ARG(tau != nullptr && ntau >= 1, 13);                                          \
   VG_CHECK_ARG(kmax >= 1 && kmax <= EX_KMAX, 15);                                         \
   VG_CHECK_ARG(cutoff >= 0, 16);                                                          \
-  VG_CHECK_ARG(qdiag != nullptr, 17);                                                     \
-  VG_CHECK_ARG(cache != nullptr, 18);                                                     \
-  VG_CHECK_ARG(selected != nullptr, 19);                                                  \
-  VG_CHECK_ARG(ws != nullptr, 20)
+  VG_CHECK_ARG(radius >= 1, 17);                                                          \
+  VG_CHECK_ARG(cg_iters >= 1 && cg_iters <= CG_MAXIT, 18);                                \
+  VG_CHECK_ARG(qdiag != nullptr, 19);                                                     \
+  VG_CHECK_ARG(cache != nullptr, 20);                                                     \
+  VG_CHECK_ARG(selected != nullptr, 21);                                                  \
+  VG_CHECK_ARG(ws != nullptr, 22)
 
 EArgs make_eargs(const double* X, int64_t I0, int64_t I1, int64_t I2, double amp, double ls,
                  double shift, double jitter, double thr, const int* offs, int m, const double* tau,
@@ -532,30 +601,35 @@ int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned
 template <int KIND>
 int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned char* sel,
                   const ExactWS& w, int round, int last, long long* picks, double* pick_delta,
-                  int cg_iters, double cg_tol, hipStream_t s) {
+                  int radius, int cg_iters, double cg_tol, hipStream_t s) {
   const long long n = a.n;
   const long long nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
-  double* x = last ? nullptr : w.Qcols + (size_t)round * n;
+  const long long bv = w.b0 * w.b1 * w.b2;
+  double* x = last ? nullptr : w.Qcols + (size_t)round * bv;
   if (x) {
-    VG_HIP(hipMemsetAsync(w.r, 0, 8 * (size_t)n, s));
-    VG_HIP(hipMemsetAsync(x, 0, 8 * (size_t)n, s));
+    VG_HIP(hipMemsetAsync(w.r, 0, 8 * (size_t)bv, s));
+    VG_HIP(hipMemsetAsync(w.p0, 0, 8 * (size_t)bv, s));
+    VG_HIP(hipMemsetAsync(w.p1, 0, 8 * (size_t)bv, s));
+    VG_HIP(hipMemsetAsync(x, 0, 8 * (size_t)bv, s));
   }
   {
     ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
-    hipLaunchKernelGGL(exact_select_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, sel, n, w, nblk,
-                       nsb, round, picks, pick_delta, x);
+    hipLaunchKernelGGL(exact_select_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, sel, a.I0, a.I1,
+                       a.I2, w, nblk, nsb, round, picks, pick_delta, x != nullptr ? 1 : 0);
     VG_LAUNCH_CHECK();
   }
   if (!x) return 0;
   {
     const int m = a.m1 + 1;
-    ProfScope ps("exact_cg", s, 0.0, (double)cg_iters * 8.0 * n * (m + 9));
+    ProfScope ps("exact_cg", s, 0.0, (double)cg_iters * 8.0 * bv * (m + 9));
     const double tol2 = cg_tol * cg_tol;
+    const unsigned blocks = (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(bv, CG_T));
     for (int it = 0; it < cg_iters; ++it) {
-      hipLaunchKernelGGL(exact_cg_a_kernel, dim3(CG_BLOCKS), dim3(CG_T), 0, s, w, a.I0, a.I1, a.I2,
-                         a.offs, a.m1, it, tol2);
+      hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I0, a.I1, a.I2,
+                         a.offs, a.m1, radius, round, picks, it, tol2);
       VG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(exact_cg_b_kernel, dim3(CG_BLOCKS), dim3(CG_T), 0, s, w, n, it, x);
+      hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I1, a.I2, radius,
+                         round, picks, it, x);
       VG_LAUNCH_CHECK();
       hipLaunchKernelGGL(exact_cg_c_kernel, dim3(1), dim3(CG_T), 0, s, w, it);
       VG_LAUNCH_CHECK();
@@ -572,21 +646,21 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
 
 }  // namespace
 
-extern "C" size_t vgposp_exact_workspace_bytes(int64_t n, int m, int kmax) {
-  if (n <= 0 || m <= 0 || kmax <= 0) return 0;
-  return exact_layout(nullptr, n, m, kmax).bytes;
+extern "C" size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
+                                               int radius, int cg_iters) {
+  if (I0 <= 0 || I1 <= 0 || I2 <= 0 || m <= 0 || kmax <= 0 || radius < 1 || cg_iters < 1) return 0;
+  return exact_layout(nullptr, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters).bytes;
 }
 
 extern "C" int vgposp_exact_prepare(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2,
                                     double amp, double ls, double diag_shift, double jitter,
                                     double threshold, const int* offsets, int m, const double* tau,
-                                    int ntau, int kmax, int cutoff, const double* qdiag,
-                                    double* cache, uint8_t* selected, void* ws, size_t ws_bytes,
-                                    void* stream) {
+                                    int ntau, int kmax, int cutoff, int radius, int cg_iters,
+                                    const double* qdiag, double* cache, uint8_t* selected, void* ws,
+                                    size_t ws_bytes, void* stream) {
   clear_error();
   VGPOSP_EXACT_CHECK_COMMON();
-  const int64_t n = I0 * I1 * I2;
-  const ExactWS w = exact_layout(ws, n, m, kmax);
+  const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);
   if (ws_bytes < w.bytes) {
     set_error("vgposp_exact_prepare: workspace %zu < %zu bytes", ws_bytes, w.bytes);
     return VGPOSP_E_WS;
@@ -605,18 +679,16 @@ extern "C" int vgposp_exact_prepare(int kind, const double* X, int64_t I0, int64
 extern "C" int vgposp_exact_round(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2,
                                   double amp, double ls, double diag_shift, double jitter,
                                   double threshold, const int* offsets, int m, const double* tau,
-                                  int ntau, int kmax, int cutoff, const double* qdiag,
-                                  double* cache, uint8_t* selected, void* ws, size_t ws_bytes,
-                                  int round, int last, int64_t* picks, double* pick_delta,
-                                  int cg_iters, double cg_tol, void* stream) {
+                                  int ntau, int kmax, int cutoff, int radius, int cg_iters,
+                                  const double* qdiag, double* cache, uint8_t* selected, void* ws,
+                                  size_t ws_bytes, int round, int last, int64_t* picks,
+                                  double* pick_delta, double cg_tol, void* stream) {
   clear_error();
   VGPOSP_EXACT_CHECK_COMMON();
-  VG_CHECK_ARG(round >= 0 && round < kmax, 22);
-  VG_CHECK_ARG(picks != nullptr, 24);
-  VG_CHECK_ARG(cg_iters >= 1 && cg_iters <= CG_MAXIT, 26);
-  VG_CHECK_ARG(cg_tol >= 0.0, 27);
-  const int64_t n = I0 * I1 * I2;
-  const ExactWS w = exact_layout(ws, n, m, kmax);
+  VG_CHECK_ARG(round >= 0 && round < kmax, 24);
+  VG_CHECK_ARG(picks != nullptr, 26);
+  VG_CHECK_ARG(cg_tol >= 0.0, 28);
+  const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);
   if (ws_bytes < w.bytes) {
     set_error("vgposp_exact_round: workspace %zu < %zu bytes", ws_bytes, w.bytes);
     return VGPOSP_E_WS;
@@ -627,22 +699,24 @@ extern "C" int vgposp_exact_round(int kind, const double* X, int64_t I0, int64_t
   long long* pk = reinterpret_cast<long long*>(picks);
   switch (kind) {
     case VGPOSP_KERNEL_EQ:
-      return exact_round_t<VGPOSP_KERNEL_EQ>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, cg_iters, cg_tol, s);
+      return exact_round_t<VGPOSP_KERNEL_EQ>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
     case VGPOSP_KERNEL_MATERN12:
-      return exact_round_t<VGPOSP_KERNEL_MATERN12>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, cg_iters, cg_tol, s);
+      return exact_round_t<VGPOSP_KERNEL_MATERN12>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
     case VGPOSP_KERNEL_MATERN32:
-      return exact_round_t<VGPOSP_KERNEL_MATERN32>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, cg_iters, cg_tol, s);
+      return exact_round_t<VGPOSP_KERNEL_MATERN32>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
     default:
-      return exact_round_t<VGPOSP_KERNEL_MATERN52>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, cg_iters, cg_tol, s);
+      return exact_round_t<VGPOSP_KERNEL_MATERN52>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
   }
 }
 
-extern "C" int vgposp_exact_buffers(void* ws, int64_t n, int m, int kmax, double** qcols,
+extern "C" int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
+                                    int radius, int cg_iters, double** qcols, int64_t** boxlo,
                                     int** cgstate) {
   clear_error();
   VG_CHECK_ARG(ws != nullptr, 1);
-  const ExactWS w = exact_layout(ws, n, m, kmax);
+  const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);
   if (qcols) *qcols = w.Qcols;
+  if (boxlo) *boxlo = reinterpret_cast<int64_t*>(w.boxlo);
   if (cgstate) *cgstate = w.cgstate;
   return 0;
 }

@@ -124,10 +124,12 @@ constexpr int XT = 64;  // square tile of the scatter / gather kernels (64 x 4 t
 
 // Parent front += child's update (lower triangle) for the children of sibling index `sib`
 // (siblings share a parent, so the two sibling passes never write the same parent concurrently).
+// Child s's parent front sits at element offsets par_off[s] of the parent LEVEL's PP / UP / UU
+// buffers, with padded sizes par_dim[s] = (p, u).
 __global__ __launch_bounds__(256) void front_extend_add_kernel(
     const double* __restrict__ UUc, int uc, const int* __restrict__ pmap,
-    const int* __restrict__ pslot, const int* __restrict__ sibl, int sib, double* PP, double* UP,
-    double* UU, int p, int u) {
+    const long long* __restrict__ par_off, const int* __restrict__ par_dim,
+    const int* __restrict__ sibl, int sib, double* PP, double* UP, double* UU) {
   const int s = blockIdx.z;
   if (sibl[s] != sib) return;
   const int bx = blockIdx.x, by = blockIdx.y;
@@ -138,8 +140,8 @@ __global__ __launch_bounds__(256) void front_extend_add_kernel(
   const int mb = m[b];
   if (mb < 0) return;
   const double* src = UUc + (size_t)s * uc * uc;
-  const int ps = pslot[s];
-  double* base[3] = {PP + (size_t)ps * p * p, UP + (size_t)ps * u * p, UU + (size_t)ps * u * u};
+  const int p = par_dim[2 * s], u = par_dim[2 * s + 1];
+  double* base[3] = {PP + par_off[3 * s], UP + par_off[3 * s + 1], UU + par_off[3 * s + 2]};
   const int a1 = min(uc, (by + 1) * XT);
   for (int aa = by * XT + (threadIdx.x >> 6); aa < a1; aa += 4) {
     if (aa < b) continue;
@@ -156,16 +158,16 @@ __global__ __launch_bounds__(256) void front_extend_add_kernel(
 // Child's full Q_UU [uc][uc] <- its parent's Q front at (pmap[a], pmap[b]); 0 on padding.
 __global__ __launch_bounds__(256) void front_gather_kernel(
     const double* __restrict__ QPP, const double* __restrict__ QUP, const double* __restrict__ QUU,
-    int p, int u, const int* __restrict__ pmap, const int* __restrict__ pslot, int uc,
-    double* __restrict__ out) {
+    const int* __restrict__ pmap, const long long* __restrict__ par_off,
+    const int* __restrict__ par_dim, int uc, double* __restrict__ out) {
   const int s = blockIdx.z;
   const int b = blockIdx.x * XT + (threadIdx.x & (XT - 1));
   if (b >= uc) return;
   const int* m = pmap + (size_t)s * uc;
   const int mb = m[b];
-  const int ps = pslot[s];
-  const double* base[3] = {QPP + (size_t)ps * p * p, QUP + (size_t)ps * u * p,
-                           QUU + (size_t)ps * u * u};
+  const int p = par_dim[2 * s], u = par_dim[2 * s + 1];
+  const double* base[3] = {QPP + par_off[3 * s], QUP + par_off[3 * s + 1],
+                           QUU + par_off[3 * s + 2]};
   double* dst = out + (size_t)s * uc * uc;
   const int a1 = min(uc, (int)(blockIdx.y + 1) * XT);
   for (int aa = blockIdx.y * XT + (threadIdx.x >> 6); aa < a1; aa += 4) {
@@ -320,41 +322,44 @@ extern "C" int vgposp_front_assemble(int kind, const double* X, int64_t I0, int6
 }
 
 extern "C" int vgposp_front_extend_add(const double* UUc, int64_t uc, int nfc, const int* pmap,
-                                       const int* pslot, const int* sibling, int sib, double* PP,
-                                       double* UP, double* UU, int64_t p, int64_t u, void* stream) {
+                                       const int64_t* par_off, const int* par_dim,
+                                       const int* sibling, int sib, double* PP, double* UP,
+                                       double* UU, void* stream) {
   clear_error();
   VG_CHECK_ARG(UUc != nullptr || uc == 0, 1);
   VG_CHECK_ARG(uc >= 0, 2);
   VG_CHECK_ARG(nfc >= 1 && nfc <= 65535, 3);
-  VG_CHECK_ARG(pmap != nullptr && pslot != nullptr && sibling != nullptr, 4);
-  VG_CHECK_ARG(PP != nullptr, 8);
-  VG_CHECK_ARG(p >= 1 && u >= 0, 11);
+  VG_CHECK_ARG(pmap != nullptr, 4);
+  VG_CHECK_ARG(par_off != nullptr && par_dim != nullptr, 5);
+  VG_CHECK_ARG(sibling != nullptr, 7);
+  VG_CHECK_ARG(PP != nullptr, 9);
   if (uc == 0) return 0;
   hipStream_t s = as_stream(stream);
   ProfScope ps("front_extend_add", s, 0.0, 8.0 * 2.0 * nfc * uc * (double)uc);
   const unsigned t = (unsigned)ceil_div(uc, XT);
   hipLaunchKernelGGL(front_extend_add_kernel, dim3(t, t, (unsigned)nfc), dim3(256), 0, s, UUc,
-                     (int)uc, pmap, pslot, sibling, sib, PP, UP, UU, (int)p, (int)u);
+                     (int)uc, pmap, reinterpret_cast<const long long*>(par_off), par_dim, sibling,
+                     sib, PP, UP, UU);
   VG_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" int vgposp_front_gather(const double* QPP, const double* QUP, const double* QUU,
-                                   int64_t p, int64_t u, const int* pmap, const int* pslot, int nfc,
-                                   int64_t uc, double* QUUc, void* stream) {
+                                   const int* pmap, const int64_t* par_off, const int* par_dim,
+                                   int nfc, int64_t uc, double* QUUc, void* stream) {
   clear_error();
   VG_CHECK_ARG(QPP != nullptr, 1);
-  VG_CHECK_ARG(p >= 1 && u >= 0, 4);
-  VG_CHECK_ARG(pmap != nullptr && pslot != nullptr, 6);
-  VG_CHECK_ARG(nfc >= 1 && nfc <= 65535, 8);
-  VG_CHECK_ARG(uc >= 0, 9);
-  VG_CHECK_ARG(QUUc != nullptr || uc == 0, 10);
+  VG_CHECK_ARG(pmap != nullptr, 4);
+  VG_CHECK_ARG(par_off != nullptr && par_dim != nullptr, 5);
+  VG_CHECK_ARG(nfc >= 1 && nfc <= 65535, 7);
+  VG_CHECK_ARG(uc >= 0, 8);
+  VG_CHECK_ARG(QUUc != nullptr || uc == 0, 9);
   if (uc == 0) return 0;
   hipStream_t s = as_stream(stream);
   ProfScope ps("front_gather", s, 0.0, 8.0 * 2.0 * nfc * uc * (double)uc);
   const unsigned t = (unsigned)ceil_div(uc, XT);
   hipLaunchKernelGGL(front_gather_kernel, dim3(t, t, (unsigned)nfc), dim3(256), 0, s, QPP, QUP, QUU,
-                     (int)p, (int)u, pmap, pslot, (int)uc, QUUc);
+                     pmap, reinterpret_cast<const long long*>(par_off), par_dim, (int)uc, QUUc);
   VG_LAUNCH_CHECK();
   return 0;
 }

@@ -71,6 +71,12 @@ class Group:
     parent_slot: np.ndarray = None   # int32 [nf]
     sibling: np.ndarray = None       # int32 [nf]
     order: np.ndarray = None         # int32 [nf] postorder id of each front
+    level: int = 0                   # index into FrontalTree.levels
+    off: tuple = (0, 0, 0)           # element offsets of this group's PP / UP / UU in its level
+    # the parent front of every front, as offsets into the parent LEVEL's PP / UP / UU buffers and
+    # its (p, u): int64 [nf, 3] and int32 [nf, 2] (-1 for a root)
+    par_off: np.ndarray = None
+    par_dim: np.ndarray = None
 
     @property
     def nf(self):
@@ -188,23 +194,35 @@ class FrontalTree:
                 raise AssertionError(f"front {i}: halo outside its ancestors")
 
     def _groups(self):
-        keys = {}
+        """Fronts of one depth form a level; a level is cut into groups of similar padded size
+        (every front of a group is padded to the group's (p, u)), largest u first, starting a new
+        group when u falls below (1 - tol) of the group's largest, so padding wastes little."""
+        tol = 0.1
+        bydepth = {}
         for i, f in enumerate(self.fronts):
-            keys.setdefault((f.depth, f.leaf), []).append(i)
-        # deepest first = a valid bottom-up processing order
-        order = sorted(keys, key=lambda k: (-k[0], not k[1]))
+            bydepth.setdefault(f.depth, []).append(i)
         self.groups: list[Group] = []
-        for gi, k in enumerate(order):
-            ids = keys[k]
-            g = Group(k[0], k[1], ids)
-            g.p_max = max(len(self.fronts[i].piv) for i in ids)
-            g.u_max = max(len(self.fronts[i].U) for i in ids)
-            g.p = _round_up(max(g.p_max, 1), self.pad)
-            g.u = _round_up(g.u_max, self.pad) if g.u_max else 0
-            for s, i in enumerate(ids):
-                self.fronts[i].group = gi
-                self.fronts[i].slot = s
-            self.groups.append(g)
+        self.levels = []            # per level: list of group indices, and total buffer sizes
+        for d in sorted(bydepth, reverse=True):          # deepest first = bottom-up order
+            ids = bydepth[d]
+            key = lambda i: (-_round_up(max(len(self.fronts[i].piv), 1), self.pad),
+                             -len(self.fronts[i].U), i)
+            ids = sorted(ids, key=key)
+            lvl = {"depth": d, "groups": [], "size": [0, 0, 0]}
+            cur = []
+            for i in ids:
+                if cur:
+                    f0 = self.fronts[cur[0]]
+                    f = self.fronts[i]
+                    same_p = (_round_up(max(len(f.piv), 1), self.pad)
+                              == _round_up(max(len(f0.piv), 1), self.pad))
+                    if not same_p or len(f.U) < (1 - tol) * len(f0.U):
+                        self._new_group(d, cur, lvl)
+                        cur = []
+                cur.append(i)
+            if cur:
+                self._new_group(d, cur, lvl)
+            self.levels.append(lvl)
         for g in self.groups:
             nf = g.nf
             g.piv = np.full((nf, g.p), -1, dtype=np.int32)
@@ -215,6 +233,8 @@ class FrontalTree:
             g.parent_slot = np.full(nf, -1, dtype=np.int32)
             g.sibling = np.zeros(nf, dtype=np.int32)
             g.order = np.asarray(g.fronts, dtype=np.int32)
+            g.par_off = np.full((nf, 3), -1, dtype=np.int64)
+            g.par_dim = np.full((nf, 2), -1, dtype=np.int32)
             for s, i in enumerate(g.fronts):
                 f = self.fronts[i]
                 g.piv[s, :len(f.piv)] = f.piv
@@ -226,6 +246,10 @@ class FrontalTree:
                     pg = self.groups[par.group]
                     g.parent_group[s] = par.group
                     g.parent_slot[s] = par.slot
+                    g.par_off[s] = (pg.off[0] + par.slot * pg.p * pg.p,
+                                    pg.off[1] + par.slot * pg.u * pg.p,
+                                    pg.off[2] + par.slot * pg.u * pg.u)
+                    g.par_dim[s] = (pg.p, pg.u)
                     own = self.owner[f.U]
                     pos = np.where(own == f.parent, self.owner_pos[f.U], -1)
                     inU = own != f.parent
@@ -235,6 +259,25 @@ class FrontalTree:
                         raise AssertionError("child boundary not inside the parent's front")
                     pos[inU] = pg.p + k
                     g.pmap[s, :len(f.U)] = pos
+
+    def _new_group(self, depth, ids, lvl):
+        gi = len(self.groups)
+        g = Group(depth, all(self.fronts[i].leaf for i in ids), list(ids))
+        g.p_max = max(len(self.fronts[i].piv) for i in ids)
+        g.u_max = max(len(self.fronts[i].U) for i in ids)
+        g.p = _round_up(max(g.p_max, 1), self.pad)
+        g.u = _round_up(g.u_max, self.pad) if g.u_max else 0
+        g.level = len(self.levels)
+        sz = lvl["size"]
+        g.off = (sz[0], sz[1], sz[2])
+        sz[0] += g.nf * g.p * g.p
+        sz[1] += g.nf * g.u * g.p
+        sz[2] += g.nf * g.u * g.u
+        for s, i in enumerate(ids):
+            self.fronts[i].group = gi
+            self.fronts[i].slot = s
+        self.groups.append(g)
+        lvl["groups"].append(gi)
 
     # ------------------------------------------------------------------ summaries
     def flops(self, padded=True):
@@ -259,6 +302,10 @@ class FrontalTree:
     def summary(self):
         return [{"depth": g.depth, "leaf": g.leaf, "fronts": g.nf, "p": g.p, "u": g.u,
                  "p_max": g.p_max, "u_max": g.u_max} for g in self.groups]
+
+    def level_bytes(self):
+        """Bytes of the PP / UP / UU buffers of every level."""
+        return [[8 * v for v in lvl["size"]] for lvl in self.levels]
 
 
 @functools.lru_cache(maxsize=8)

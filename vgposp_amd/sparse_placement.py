@@ -107,79 +107,90 @@ class FrontalSelectedInverse:
         for g in T.groups:
             self.g.append({
                 "piv": _dev(g.piv, dev), "U": _dev(g.U, dev), "ulen": _dev(g.ulen, dev),
-                "pmap": _dev(g.pmap, dev), "pslot": _dev(g.parent_slot, dev),
-                "sib": _dev(g.sibling, dev), "order": _dev(g.order, dev)})
-        self.children = {i: [] for i in range(len(T.groups))}
-        self.parent = {}
-        for ci, g in enumerate(T.groups):
-            pg = np.unique(g.parent_group)
-            if len(pg) != 1:
-                raise AssertionError("a group's fronts must share one parent group")
-            if pg[0] >= 0:
-                self.children[int(pg[0])].append(ci)
-                self.parent[ci] = int(pg[0])
+                "pmap": _dev(g.pmap, dev), "par_off": _dev(g.par_off, dev, torch.int64),
+                "par_dim": _dev(g.par_dim, dev), "sib": _dev(g.sibling, dev),
+                "order": _dev(g.order, dev)})
         self.infos = []
 
     def flops(self):
         return self.tree.flops(padded=True)
 
-    def run(self, out=None):
-        """-> qdiag [N] (device).  Cholesky status per group in ``self.infos`` (device)."""
+    def run(self, out=None, timer=None):
+        """-> qdiag [N] (device).  Cholesky status per group in ``self.infos`` (device).
+        ``timer`` (callable(tag)) is called between phases (e.g. to record events).
+
+        Storage is per tree level: three flat buffers (PP, UP, UU) holding the level's groups at
+        their plan offsets; a child's parent is addressed by its static offsets into the parent
+        level's buffers (nested_dissection.Group.par_off)."""
         prob, T = self.p, self.tree
+        tick = timer if timer is not None else (lambda tag: None)
         dev = prob.device
         f64 = torch.float64
         G = T.groups
-        store = [None] * len(G)
-        uu = [None] * len(G)
+        L = T.levels
+        store = [None] * len(L)
+        uu_prev = None
         self.infos = []
-        for gi, g in enumerate(G):
-            d = self.g[gi]
-            PP = torch.zeros((g.nf, g.p, g.p), dtype=f64, device=dev)
-            UP = torch.zeros((g.nf, g.u, g.p), dtype=f64, device=dev) if g.u else None
-            UU = torch.zeros((g.nf, g.u, g.u), dtype=f64, device=dev) if g.u else None
-            call("vgposp_front_assemble", *prob.taper_args(), _p(prob.offs), prob.m, _p(prob.tau),
-                 prob.tau.numel(), _p(self.owner_ord), _p(self.owner_pos), _p(d["piv"]), g.p,
-                 _p(d["U"]), g.u, _p(d["ulen"]), _p(d["order"]), g.nf, _p(PP), _p(UP), _stream())
-            for ci in self.children[gi]:
-                c, cd = G[ci], self.g[ci]
-                for sib in (0, 1):
-                    call("vgposp_front_extend_add", _p(uu[ci]), c.u, c.nf, _p(cd["pmap"]),
-                         _p(cd["pslot"]), _p(cd["sib"]), sib, _p(PP), _p(UP), _p(UU), g.p, g.u,
-                         _stream())
-                uu[ci] = None
-            info = torch.empty(g.nf, dtype=I32, device=dev)
-            ws = torch.empty(query("vgposp_front_factor_workspace_bytes", g.p, g.u, g.nf),
-                             dtype=torch.uint8, device=dev)
-            call("vgposp_front_factor", _p(PP), _p(UP), _p(UU), g.p, g.u, g.nf, _p(info), _p(ws),
-                 ws.numel(), _stream())
-            del ws
-            self.infos.append(info)
-            store[gi] = (PP, UP)
-            uu[gi] = UU
+        tick(("start", -1))
+        for li, lvl in enumerate(L):
+            s0, s1, s2 = lvl["size"]
+            PP = torch.zeros(max(s0, 1), dtype=f64, device=dev)
+            UP = torch.zeros(max(s1, 1), dtype=f64, device=dev)
+            UU = torch.zeros(max(s2, 1), dtype=f64, device=dev)
+            for gi in lvl["groups"]:
+                g, d = G[gi], self.g[gi]
+                call("vgposp_front_assemble", *prob.taper_args(), _p(prob.offs), prob.m,
+                     _p(prob.tau), prob.tau.numel(), _p(self.owner_ord), _p(self.owner_pos),
+                     _p(d["piv"]), g.p, _p(d["U"]), g.u, _p(d["ulen"]), _p(d["order"]), g.nf,
+                     _p(PP[g.off[0]:]), _p(UP[g.off[1]:]), _stream())
+            if li > 0:
+                for ci in L[li - 1]["groups"]:
+                    c, cd = G[ci], self.g[ci]
+                    if not c.u:
+                        continue
+                    for sib in (0, 1):
+                        call("vgposp_front_extend_add", _p(uu_prev[c.off[2]:]), c.u, c.nf,
+                             _p(cd["pmap"]), _p(cd["par_off"]), _p(cd["par_dim"]), _p(cd["sib"]),
+                             sib, _p(PP), _p(UP), _p(UU), _stream())
+            uu_prev = None
+            for gi in lvl["groups"]:
+                g = G[gi]
+                info = torch.empty(g.nf, dtype=I32, device=dev)
+                ws = torch.empty(query("vgposp_front_factor_workspace_bytes", g.p, g.u, g.nf),
+                                 dtype=torch.uint8, device=dev)
+                call("vgposp_front_factor", _p(PP[g.off[0]:]), _p(UP[g.off[1]:] if g.u else None),
+                     _p(UU[g.off[2]:] if g.u else None), g.p, g.u, g.nf, _p(info), _p(ws),
+                     ws.numel(), _stream())
+                del ws
+                self.infos.append(info)
+            tick(("factor", li))
+            store[li] = (PP, UP)
+            uu_prev = UU
+        del uu_prev
         qdiag = out if out is not None else torch.empty(prob.n, dtype=f64, device=dev)
-        Q = [None] * len(G)
-        left = {i: len(self.children[i]) for i in range(len(G))}
-        for gi in range(len(G) - 1, -1, -1):
-            g, d = G[gi], self.g[gi]
-            M, W = store[gi]
-            QUU = None
-            if g.u:
-                pg = self.parent[gi]
-                QPPp, QUPp, QUUp = Q[pg]
-                QUU = torch.empty((g.nf, g.u, g.u), dtype=f64, device=dev)
-                call("vgposp_front_gather", _p(QPPp), _p(QUPp), _p(QUUp), G[pg].p, G[pg].u,
-                     _p(d["pmap"]), _p(d["pslot"]), g.nf, g.u, _p(QUU), _stream())
-                left[pg] -= 1
-                if left[pg] == 0:
-                    Q[pg] = None
-            QPP = torch.empty((g.nf, g.p, g.p), dtype=f64, device=dev)
-            QUP = torch.empty((g.nf, g.u, g.p), dtype=f64, device=dev) if g.u else None
-            call("vgposp_front_selinv", _p(M), _p(W), _p(QUU), g.p, g.u, g.nf, _p(QPP), _p(QUP),
-                 _stream())
-            store[gi] = None
+        Qpar = None
+        for li in range(len(L) - 1, -1, -1):
+            lvl = L[li]
+            s0, s1, s2 = lvl["size"]
+            M, W = store[li]
+            QPP = torch.empty(max(s0, 1), dtype=f64, device=dev)
+            QUP = torch.empty(max(s1, 1), dtype=f64, device=dev)
+            QUU = torch.empty(max(s2, 1), dtype=f64, device=dev)
+            for gi in lvl["groups"]:
+                g, d = G[gi], self.g[gi]
+                if g.u:
+                    call("vgposp_front_gather", _p(Qpar[0]), _p(Qpar[1]), _p(Qpar[2]),
+                         _p(d["pmap"]), _p(d["par_off"]), _p(d["par_dim"]), g.nf, g.u,
+                         _p(QUU[g.off[2]:]), _stream())
+                call("vgposp_front_selinv", _p(M[g.off[0]:]), _p(W[g.off[1]:] if g.u else None),
+                     _p(QUU[g.off[2]:] if g.u else None), g.p, g.u, g.nf, _p(QPP[g.off[0]:]),
+                     _p(QUP[g.off[1]:] if g.u else None), _stream())
+                call("vgposp_front_diag", _p(QPP[g.off[0]:]), g.p, g.nf, _p(d["piv"]), _p(qdiag),
+                     _stream())
+            store[li] = None
             del M, W
-            call("vgposp_front_diag", _p(QPP), g.p, g.nf, _p(d["piv"]), _p(qdiag), _stream())
-            Q[gi] = (QPP, QUP, QUU) if self.children[gi] else None
+            Qpar = (QPP, QUP, QUU)
+            tick(("selinv", li))
         return qdiag
 
     def check(self):
@@ -200,20 +211,22 @@ class ExactWindowGreedy:
         self.kmax, self.cutoff = int(kmax), int(cutoff)
         dev = prob.device
         n = prob.n
+        self.radius = max(int(np.abs(prob.offs_np).max()) if len(prob.offs_np) else 1, 1)
         self.cache = torch.zeros(n, dtype=torch.float64, device=dev)
         self.selected = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.picks = torch.full((self.kmax,), -1, dtype=torch.int64, device=dev)
         self.pick_delta = torch.zeros(self.kmax, dtype=torch.float64, device=dev)
-        self.ws = torch.empty(query("vgposp_exact_workspace_bytes", n, prob.m, self.kmax),
-                              dtype=torch.uint8, device=dev)
         self.cg_tol = float(cg_tol)
         self.cg_iters = int(cg_iters) if cg_iters else prob.cg_iterations(cg_tol)
+        self.box = [min(2 * self.radius * self.cg_iters + 1, s) for s in prob.shape]
+        self.ws = torch.empty(query("vgposp_exact_workspace_bytes", *prob.shape, prob.m, self.kmax,
+                                    self.radius, self.cg_iters), dtype=torch.uint8, device=dev)
 
     def _args(self, qdiag):
         pr = self.p
         return (*pr.taper_args(), pr.thr, _p(pr.offs), pr.m, _p(pr.tau), pr.tau.numel(),
-                self.kmax, self.cutoff, _p(qdiag), _p(self.cache), _p(self.selected), _p(self.ws),
-                self.ws.numel())
+                self.kmax, self.cutoff, self.radius, self.cg_iters, _p(qdiag), _p(self.cache),
+                _p(self.selected), _p(self.ws), self.ws.numel())
 
     def run(self, qdiag, k, snapshots=None):
         """snippets_a3.py:43-364 -> picks [k] (device).  ``snapshots`` (list) receives the cache
@@ -227,27 +240,35 @@ class ExactWindowGreedy:
         for t in range(k):
             last = t == k - 1
             call("vgposp_exact_round", *self._args(qdiag), t, int(last), _p(self.picks),
-                 _p(self.pick_delta), self.cg_iters, self.cg_tol, _stream())
+                 _p(self.pick_delta), self.cg_tol, _stream())
             if snapshots is not None and not last:
                 snapshots.append(self.cache.clone())
         return self.picks[:k]
 
     def _buffers(self):
-        q, c = ctypes.c_void_p(), ctypes.c_void_p()
-        call("vgposp_exact_buffers", _p(self.ws), self.p.n, self.p.m, self.kmax, ctypes.byref(q),
-             ctypes.byref(c))
-        return q.value - self.ws.data_ptr(), c.value - self.ws.data_ptr()
+        q, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        call("vgposp_exact_buffers", _p(self.ws), *self.p.shape, self.p.m, self.kmax, self.radius,
+             self.cg_iters, ctypes.byref(q), ctypes.byref(b), ctypes.byref(c))
+        base = self.ws.data_ptr()
+        return q.value - base, b.value - base, c.value - base
 
     def q_columns(self):
-        """The CG columns Q e_{a_t} [kmax][N] (a view into the workspace)."""
-        off, _ = self._buffers()
-        n = self.p.n
-        return self.ws[off: off + 8 * self.kmax * n].view(torch.float64).view(self.kmax, n)
+        """The CG columns Q e_{a_t} expanded to the grid: [kmax, N] (zero outside each box)."""
+        qo, bo, _ = self._buffers()
+        b0, b1, b2 = self.box
+        bv = b0 * b1 * b2
+        cols = self.ws[qo: qo + 8 * self.kmax * bv].view(torch.float64).view(self.kmax, b0, b1, b2)
+        lo = self.ws[bo: bo + 8 * 3 * self.kmax].view(torch.int64).view(self.kmax, 3).cpu()
+        full = torch.zeros((self.kmax,) + self.p.shape, dtype=torch.float64, device=self.ws.device)
+        for t in range(self.kmax):
+            l0, l1, l2 = (int(v) for v in lo[t])
+            full[t, l0:l0 + b0, l1:l1 + b1, l2:l2 + b2] = cols[t]
+        return full.view(self.kmax, -1)
 
     def cg_iterations_used(self):
-        """Iterations the last CG solve took (0 if it ran the full budget without converging)."""
-        _, off = self._buffers()
-        st = self.ws[off: off + 8].view(torch.int32)
+        """Iterations the last CG solve took (the full budget if it did not stop early)."""
+        _, _, co = self._buffers()
+        st = self.ws[co: co + 8].view(torch.int32)
         return int(st[1]) if int(st[0]) else self.cg_iters
 
 
