@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                         "the multi-rank path on one GPU with VGPOSP_BENCH_DEVICE=0)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r1.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r3.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
 
@@ -106,10 +106,31 @@ def cpu_baseline(args, N):
 
     shape = (16, 16, 32)
     S = sigma(shape)
-    t0 = time.perf_counter()
-    op.placement_lazy_incremental(S, args.k)
-    t_inc = time.perf_counter() - t0
+    # all the host's logical CPUs (OPENBLAS_NUM_THREADS = os.cpu_count()), and the
+    # CPUs this process may run on (the GPU box gives each GPU a share of the machine)
+    runs = {}
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits = None
+    ncpu = os.cpu_count() or 1
+    try:
+        naff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        naff = ncpu
+    for th in sorted({ncpu, naff}, reverse=True):
+        if threadpool_limits is not None:
+            with threadpool_limits(limits=th, user_api="blas"):
+                t0 = time.perf_counter()
+                op.placement_lazy_incremental(S, args.k)
+                runs[th] = time.perf_counter() - t0
+        else:
+            t0 = time.perf_counter()
+            op.placement_lazy_incremental(S, args.k)
+            runs[cpu_threads()] = time.perf_counter() - t0
     del S
+    th_main = max(runs)
+    t_inc = runs[th_main]
     ps = tuple(args.cpu_shape)
     Sp = sigma(ps)
     trace = []
@@ -126,7 +147,10 @@ def cpu_baseline(args, N):
     return {
         "value": args.k / t_inc,
         "unit": "placements/s",
-        "cores": cpu_threads(),
+        "cores": th_main,
+        "os_cpu_count": ncpu,
+        "affinity_cpus": naff,
+        "by_threads": {str(t): args.k / v for t, v in runs.items()},
         "kind": "port",
         "sample": (f"oracle placement_lazy_incremental (same algorithm as the GPU path) on a "
                    f"jittered {shape[0]}x{shape[1]}x{shape[2]} grid (N={n_inc}), k={args.k}: "
@@ -146,7 +170,9 @@ def cpu_baseline(args, N):
 def load_traffic(path, kernel, N, shape, k):
     """Per-launch HBM bytes of `kernel` measured by a rocprofv3 PMC pass of this same workload
     (tools/pmc_traffic.py writes the file; (FETCH_SIZE x 2 + WRITE_SIZE) x 1024 per the gfx950
-    correction in MI355X_MICROARCH.md).  None when absent or measured on another workload."""
+    correction in MI355X_MICROARCH.md).  None when absent, measured on another workload, or
+    measured on a build whose kernel sources differ from this one's (source_sha256)."""
+    from vgposp_amd._lib import source_hash
     try:
         with open(path) as f:
             t = json.load(f)
@@ -158,6 +184,9 @@ def load_traffic(path, kernel, N, shape, k):
     kern = t.get("kernels", {}).get(kernel)
     if not kern:
         return None
+    if kern.get("source_sha256") != source_hash(kernel):
+        return {"stale": True, "source": os.path.relpath(path, ROOT),
+                "recorded_sha256": kern.get("source_sha256"), "build_sha256": source_hash(kernel)}
     return {"bytes_per_launch": kern["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
 
 
@@ -512,6 +541,10 @@ def main():
                  "measured": "HIP events around every launch on the library's stream, in one extra "
                              "profiled step after the timed loop"})
     tr = load_traffic(args.traffic, dom, N, shape, k)
+    if tr is not None and tr.get("stale"):
+        roof["traffic_note"] = (f"null: {tr['source']} was measured on kernel sources "
+                                f"{tr['recorded_sha256']}, this build is {tr['build_sha256']}")
+        tr = None
     if tr is not None:
         roof["traffic"] = tr["bytes_per_launch"]
         roof["traffic_vs_algorithmic"] = tr["bytes_per_launch"] / (nbytes / max(launches, 1))
@@ -527,6 +560,10 @@ def main():
     if hbm["achieved"] is not None:
         hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
     trm = load_traffic(args.traffic, "greedy_trmv", N, shape, k)
+    if trm is not None and trm.get("stale"):
+        hbm["traffic_note"] = (f"null: {trm['source']} was measured on kernel sources "
+                               f"{trm['recorded_sha256']}, this build is {trm['build_sha256']}")
+        trm = None
     if trm is not None and n_t and by_t:
         hbm["traffic"] = trm["bytes_per_launch"]
         hbm["traffic_vs_algorithmic"] = trm["bytes_per_launch"] / (by_t / n_t)

@@ -118,3 +118,47 @@ def test_exact_alg3_matches_dense_engine(n):
     del S
     torch.cuda.empty_cache()
     assert [int(a) for a in A] == [int(a) for a in dense]
+
+
+def _two_rank_worker(rank, world, port, shape, k, out):
+    import os
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vgposp_amd.sparse_placement import tapered_placement_algorithm_3
+        X, ls = _grid(shape, seed=4)
+        A, d, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
+                                                leaf=128)
+        out[rank] = ([int(a) for a in A], [float(v) for v in d])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_exact_alg3_ranks_on_one_gpu(world):
+    """The multi-rank C4 path (subtree-to-subcube selected inverse, transfers host-staged over
+    gloo, every rank on cuda:0) gives the single-rank picks and deltas bit for bit."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from vgposp_amd.sparse_placement import tapered_placement_algorithm_3
+    shape, k = (16, 14, 12), 20
+    X, ls = _grid(shape, seed=4)
+    A1, d1, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
+                                              leaf=128)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    mp.start_processes(_two_rank_worker, args=(world, port, shape, k, out), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        assert out[r][0] == [int(a) for a in A1]
+        np.testing.assert_allclose(out[r][1], d1, rtol=1e-13)

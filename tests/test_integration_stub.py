@@ -38,3 +38,19 @@ def test_stub_matches_golden(name):
     assert [int(a) for a in ns["placement_algorithm_2"](cov, e["k"])] == e["alg2"]
     if "alg1" in e:
         assert [int(a) for a in ns["placement_algorithm_1"](cov, e["k"])] == e["alg1"]
+
+
+@pytest.mark.gpu
+def test_stub_singular_cov_retries():
+    import numpy as np
+    from vgposp_amd.placement_algorithm2 import placement_algorithm_2
+    ns = _stub_namespace()
+    rng = np.random.default_rng(3)
+    X = rng.uniform(-1, 1, (40, 3))
+    X[7] = X[3]                                   # duplicated location: rank-deficient kernel
+    K = np.exp(-0.5 * ((X[:, None] - X[None]) ** 2).sum(-1) / 0.3 ** 2)
+    T = rng.normal(size=(60, 12))                 # 12 samples < 60 locations
+    E = np.cov(T)
+    for cov in (K, E):
+        want = [int(a) for a in placement_algorithm_2(cov, 6)]
+        assert [int(a) for a in ns["placement_algorithm_2"](cov, 6)] == want

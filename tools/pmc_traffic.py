@@ -59,11 +59,16 @@ def main():
         cat = category(name)
         if cat:
             agg[cat][1] += wv[d]
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from vgposp_amd._lib import source_hash
     kernels = {}
     for cat, (fetch, write, n) in agg.items():
         kernels[cat] = {"launches": n, "fetch_kib_per_launch": fetch / n,
                         "write_kib_per_launch": write / n,
-                        "hbm_bytes_per_launch": (2.0 * fetch + write) * 1024.0 / n}
+                        "hbm_bytes_per_launch": (2.0 * fetch + write) * 1024.0 / n,
+                        "source_sha256": source_hash(cat)}
     out = {"workload": {"N": a.N, "shape": a.shape, "k": a.k}, "command": a.command,
            "formula": "(FETCH_SIZE * 2 + WRITE_SIZE) * 1024 per dispatch, averaged per kernel",
            "kernels": kernels}

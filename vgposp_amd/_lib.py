@@ -247,6 +247,26 @@ def query(name, *args):
     return int(getattr(load(), name)(*args))
 
 
+# source files whose compiled code each profiled kernel family runs (for matching PMC traffic
+# records to the build they were measured on)
+KERNEL_SOURCES = {
+    "gemm_f64": ["gemm.hip", "common.h", "Makefile"],
+    "greedy_trmv": ["greedy.hip", "common.h", "Makefile"],
+    "greedy_colsq": ["greedy.hip", "common.h", "Makefile"],
+    "kernel_matrix": ["kernel_matrix.hip", "psd.h", "common.h", "Makefile"],
+}
+
+
+def source_hash(kernel):
+    """sha256 (16 hex digits) of the sources a kernel family is compiled from."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES.get(kernel, []):
+        with open(os.path.join(_HERE, "csrc", name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 _prof_state = [False]
 
 

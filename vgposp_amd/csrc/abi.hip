@@ -126,3 +126,66 @@ extern "C" int64_t vgposp_prof_dump(char* buf, size_t len) {
   }
   return (int64_t)out.size() + 1;
 }
+
+namespace vgposp {
+
+__global__ void vg_fill_bytes_kernel(unsigned char* p, size_t n, unsigned char v) {
+  // 8 bytes per thread where aligned, bytes at the ends
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t head = (8 - (reinterpret_cast<uintptr_t>(p) & 7)) & 7;
+  if (i < head && i < n) p[i] = v;
+  const size_t n8 = n > head ? (n - head) / 8 : 0;
+  unsigned long long w = v;
+  w |= w << 8;
+  w |= w << 16;
+  w |= w << 32;
+  for (size_t k = i; k < n8; k += (size_t)gridDim.x * blockDim.x)
+    reinterpret_cast<unsigned long long*>(p + head)[k] = w;
+  const size_t t0 = head + 8 * n8;
+  if (t0 + i < n && i < 8) p[t0 + i] = v;
+}
+
+__global__ void vg_copy2d_kernel(unsigned char* dst, size_t dpitch, const unsigned char* src,
+                                 size_t spitch, size_t width, size_t height) {
+  const size_t row = blockIdx.y;
+  if (row >= height) return;
+  unsigned char* d = dst + row * dpitch;
+  const unsigned char* sp = src + row * spitch;
+  const bool w8 = ((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(sp) | width) & 7) == 0;
+  if (w8) {
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < width / 8;
+         k += (size_t)gridDim.x * blockDim.x)
+      reinterpret_cast<double*>(d)[k] = reinterpret_cast<const double*>(sp)[k];
+  } else {
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < width;
+         k += (size_t)gridDim.x * blockDim.x)
+      d[k] = sp[k];
+  }
+}
+
+hipError_t vg_memset(void* p, int value, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  const size_t blocks = std::min<size_t>((bytes / 8 + 255) / 256 + 1, 4096);
+  hipLaunchKernelGGL(vg_fill_bytes_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                     static_cast<unsigned char*>(p), bytes, (unsigned char)value);
+  return hipGetLastError();
+}
+
+hipError_t vg_memcpy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                       size_t height, hipMemcpyKind kind, hipStream_t s) {
+  if (kind != hipMemcpyDeviceToDevice)
+    return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, kind, s);
+  if (width == 0 || height == 0) return hipSuccess;
+  size_t bx = std::min<size_t>((width / 8 + 255) / 256, 64);
+  if (bx == 0) bx = 1;
+  for (size_t r0 = 0; r0 < height; r0 += 65535) {
+    const size_t h = std::min<size_t>(height - r0, 65535);
+    hipLaunchKernelGGL(vg_copy2d_kernel, dim3((unsigned)bx, (unsigned)h), dim3(256), 0, s,
+                       static_cast<unsigned char*>(dst) + r0 * dpitch,
+                       dpitch, static_cast<const unsigned char*>(src) + r0 * spitch, spitch,
+                       width, h);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace vgposp

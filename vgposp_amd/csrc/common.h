@@ -38,6 +38,18 @@ void clear_error();
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Device-to-device fills and 2-D copies as KERNELS (same signatures as hipMemsetAsync /
+// hipMemcpy2DAsync).  Everything the library enqueues is then a kernel node when a caller
+// captures it into a HIP graph (the VGP training step): replays of captured memset / memcpy
+// nodes were the one ordering hazard seen on this ROCm build (a status buffer read after a replay
+// returned stale data unless the host synchronised first).
+__global__ void vg_fill_bytes_kernel(unsigned char* p, size_t n, unsigned char v);
+__global__ void vg_copy2d_kernel(unsigned char* dst, size_t dpitch, const unsigned char* src,
+                                 size_t spitch, size_t width, size_t height);
+hipError_t vg_memset(void* p, int value, size_t bytes, hipStream_t s);
+hipError_t vg_memcpy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                       size_t height, hipMemcpyKind kind, hipStream_t s);
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---- device helpers -------------------------------------------------------------------------

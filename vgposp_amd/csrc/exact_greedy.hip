@@ -295,11 +295,11 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
   if (wave == 0) wave_super_key(w.bval, w.bidx, nblk, b / ESB, w.sval, w.sidx);
 }
 
-// Deterministic block reduction of CG_BLOCKS partials (every block computes the same sum).
-__device__ __forceinline__ double sum_partials(const double* part, double* red) {
+// Deterministic block reduction of the first `np` partials (every block computes the same sum).
+__device__ __forceinline__ double sum_partials(const double* part, int np, double* red) {
   const int t = threadIdx.x;
   double s = 0.0;
-  for (int i = t; i < CG_BLOCKS; i += CG_T) s += part[i];
+  for (int i = t; i < np; i += CG_T) s += part[i];
   s = wave_sum(s);
   if ((t & 63) == 0) red[t >> 6] = s;
   __syncthreads();
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
                                                           double* __restrict__ x) {
   __shared__ double red[CG_T / 64];
   if (w.cgstate[0]) return;
-  const double pq = sum_partials(w.part_pq, red);
+  const double pq = sum_partials(w.part_pq, (int)gridDim.x, red);  // the A kernel's grid
   const double alpha = w.rr[it] / pq;
   const double* p = (it & 1) ? w.p1 : w.p0;
   const long long a = picks[round];
@@ -421,10 +421,10 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
 }
 
 // |r|^2 of iteration it + 1 (one block; every CG_A block then reads it).
-__global__ __launch_bounds__(CG_T) void exact_cg_c_kernel(ExactWS w, int it) {
+__global__ __launch_bounds__(CG_T) void exact_cg_c_kernel(ExactWS w, int it, int np) {
   __shared__ double red[CG_T / 64];
   if (w.cgstate[0]) return;
-  const double rr = sum_partials(w.part_rr, red);
+  const double rr = sum_partials(w.part_rr, np, red);
   if (threadIdx.x == 0) w.rr[it + 1] = rr;
 }
 
@@ -579,7 +579,7 @@ int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned
                     const ExactWS& w, hipStream_t s) {
   const long long n = a.n;
   const long long nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
-  VG_HIP(hipMemsetAsync(sel, 0, n, s));
+  VG_HIP(vg_memset(sel, 0, n, s));
   hipLaunchKernelGGL(exact_coef_kernel<KIND>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, a,
                      w.coef);
   VG_LAUNCH_CHECK();
@@ -607,10 +607,10 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
   const long long bv = w.b0 * w.b1 * w.b2;
   double* x = last ? nullptr : w.Qcols + (size_t)round * bv;
   if (x) {
-    VG_HIP(hipMemsetAsync(w.r, 0, 8 * (size_t)bv, s));
-    VG_HIP(hipMemsetAsync(w.p0, 0, 8 * (size_t)bv, s));
-    VG_HIP(hipMemsetAsync(w.p1, 0, 8 * (size_t)bv, s));
-    VG_HIP(hipMemsetAsync(x, 0, 8 * (size_t)bv, s));
+    VG_HIP(vg_memset(w.r, 0, 8 * (size_t)bv, s));
+    VG_HIP(vg_memset(w.p0, 0, 8 * (size_t)bv, s));
+    VG_HIP(vg_memset(w.p1, 0, 8 * (size_t)bv, s));
+    VG_HIP(vg_memset(x, 0, 8 * (size_t)bv, s));
   }
   {
     ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
@@ -631,7 +631,7 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
       hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I1, a.I2, radius,
                          round, picks, it, x);
       VG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(exact_cg_c_kernel, dim3(1), dim3(CG_T), 0, s, w, it);
+      hipLaunchKernelGGL(exact_cg_c_kernel, dim3(1), dim3(CG_T), 0, s, w, it, (int)blocks);
       VG_LAUNCH_CHECK();
     }
   }

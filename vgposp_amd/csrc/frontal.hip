@@ -226,7 +226,7 @@ extern "C" int vgposp_front_factor(double* PP, double* UP, double* UU, int64_t p
     return VGPOSP_E_WS;
   }
   hipStream_t s = as_stream(stream);
-  VG_HIP(hipMemsetAsync(info, 0, sizeof(int) * nf, s));
+  VG_HIP(vg_memset(info, 0, sizeof(int) * nf, s));
   const bool part = front_use_part(nf);
   char* w = static_cast<char*>(ws);
   double* tmp = reinterpret_cast<double*>(w + falign(potrf_ws_bytes_opt(p, part) * nf));

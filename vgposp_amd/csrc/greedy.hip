@@ -467,7 +467,7 @@ extern "C" int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int 
     return VGPOSP_E_WS;
   }
   hipStream_t s = as_stream(stream);
-  VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
+  VG_HIP(vg_memset(info, 0, sizeof(int), s));
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
                      n, lda, jitter, threshold, cache_init, w);
   VG_LAUNCH_CHECK();
@@ -613,7 +613,7 @@ extern "C" int vgposp_greedy_prepare(double* Sigma, int64_t n, int64_t lda, int 
                              ws, ws_bytes, &w))
     return rc;
   hipStream_t s = as_stream(stream);
-  VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
+  VG_HIP(vg_memset(info, 0, sizeof(int), s));
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
                      n, lda, jitter, threshold, cache_init, w);
   VG_LAUNCH_CHECK();

@@ -415,7 +415,7 @@ static int trsm_rec(const Fact& f, double* B, int64_t m, int64_t ldb, const doub
                     VGPOSP_FULL, 0, 1)))
       return rc;
     for (int b = 0; b < f.batch; ++b)
-      VG_HIP(hipMemcpy2DAsync(B + b * f.stride(B), ldb * sizeof(double), f.tmp + b * f.sW,
+      VG_HIP(vg_memcpy2d(B + b * f.stride(B), ldb * sizeof(double), f.tmp + b * f.sW,
                               NBI * sizeof(double), nL * sizeof(double), m,
                               hipMemcpyDeviceToDevice, f.s));
     return 0;
@@ -603,7 +603,7 @@ int partial_inverse(double* A, int64_t n, int64_t lda, int64_t c0, int64_t c1, d
     return rc;
   // tmp <- L22^-1 tmp
   if ((rc = trsm_left_rec(f, A + c1 * lda + c1, lda, m2, c1, 0, tmp, w, w))) return rc;
-  VG_HIP(hipMemcpy2DAsync(L21, lda * sizeof(double), tmp, w * sizeof(double), w * sizeof(double),
+  VG_HIP(vg_memcpy2d(L21, lda * sizeof(double), tmp, w * sizeof(double), w * sizeof(double),
                           m2, hipMemcpyDeviceToDevice, s));
   return 0;
 }
@@ -678,10 +678,10 @@ int pack_rows(double* A, int64_t lda, int64_t r0, int64_t r1, int64_t c0, int64_
   if (!lower) {
     const size_t w = (size_t)(c1 - c0) * sizeof(double);
     if (unpack)
-      VG_HIP(hipMemcpy2DAsync(A + r0 * lda + c0, lda * sizeof(double), buf, w, w, m,
+      VG_HIP(vg_memcpy2d(A + r0 * lda + c0, lda * sizeof(double), buf, w, w, m,
                               hipMemcpyDeviceToDevice, s));
     else
-      VG_HIP(hipMemcpy2DAsync(buf, w, A + r0 * lda + c0, lda * sizeof(double), w, m,
+      VG_HIP(vg_memcpy2d(buf, w, A + r0 * lda + c0, lda * sizeof(double), w, m,
                               hipMemcpyDeviceToDevice, s));
     return 0;
   }
@@ -705,7 +705,7 @@ static int trsm_left_rec(const Fact& f, const double* Lp, int64_t ldl, int64_t n
     if ((rc = pgemm(f, trans, 0, n, m, n, 1.0, f.leaf(col0), NB, B, ldb, 0.0, f.tmp, m,
                     VGPOSP_FULL, 0, 0)))
       return rc;
-    VG_HIP(hipMemcpy2DAsync(B, ldb * sizeof(double), f.tmp, m * sizeof(double), m * sizeof(double),
+    VG_HIP(vg_memcpy2d(B, ldb * sizeof(double), f.tmp, m * sizeof(double), m * sizeof(double),
                             n, hipMemcpyDeviceToDevice, f.s));
     return 0;
   }
@@ -803,7 +803,7 @@ extern "C" int vgposp_potrf_lower(double* A, int64_t n, int64_t lda, int64_t str
   VG_CHECK_ARG(info != nullptr, 8);
   VG_CHECK_ARG(ws != nullptr || n == 0, 9);
   hipStream_t s = as_stream(stream);
-  VG_HIP(hipMemsetAsync(info, 0, sizeof(int) * batch, s));
+  VG_HIP(vg_memset(info, 0, sizeof(int) * batch, s));
   if (n == 0) return 0;
   if (ws_bytes < potrf_ws_bytes(n)) {
     set_error("vgposp_potrf_lower: workspace %zu < %zu bytes", ws_bytes, potrf_ws_bytes(n));

@@ -257,7 +257,7 @@ static int spotrf(const MixedWS& w, int64_t n, int* info, hipStream_t s) {
     int rc;
     // tmp = P Linv^T  (Linv [jb][jb] at pitch SNB), then back into the panel
     if ((rc = sgemm_nt(rest, jb, jb, 1.0f, P, n, Lj, SNB, 0.0f, w.tmp, jb, 0, s))) return rc;
-    VG_HIP(hipMemcpy2DAsync(P, n * sizeof(float), w.tmp, jb * sizeof(float), jb * sizeof(float),
+    VG_HIP(vg_memcpy2d(P, n * sizeof(float), w.tmp, jb * sizeof(float), jb * sizeof(float),
                             rest, hipMemcpyDeviceToDevice, s));
     // trailing A22 -= P P^T (lower)
     if ((rc = sgemm_nt(rest, rest, jb, -1.0f, w.tmp, jb, w.tmp, jb, 1.0f, P + jb, n, 1, s)))
@@ -292,8 +292,8 @@ extern "C" int vgposp_potrf_mixed(const double* A, int64_t n, int64_t lda, doubl
     return VGPOSP_E_WS;
   }
   hipStream_t s = as_stream(stream);
-  VG_HIP(hipMemsetAsync(info, 0, sizeof(int), s));
-  VG_HIP(hipMemsetAsync(w.amax, 0, sizeof(unsigned long long), s));
+  VG_HIP(vg_memset(info, 0, sizeof(int), s));
+  VG_HIP(vg_memset(w.amax, 0, sizeof(unsigned long long), s));
   hipLaunchKernelGGL(cast_lower_kernel, dim3(1, (unsigned)n), dim3(256), 0, s, A, lda, w.A32, n);
   VG_LAUNCH_CHECK();
   int rc = spotrf(w, n, info, s);
@@ -303,18 +303,18 @@ extern "C" int vgposp_potrf_mixed(const double* A, int64_t n, int64_t lda, doubl
   hipLaunchKernelGGL(upcast_lower_kernel, dim3(1, (unsigned)n), dim3(256), 0, s, w.A32, n, w.T, n,
                      w.E);
   VG_LAUNCH_CHECK();
-  VG_HIP(hipMemcpy2DAsync(X, ldl * sizeof(double), w.E, n * sizeof(double), n * sizeof(double), n,
+  VG_HIP(vg_memcpy2d(X, ldl * sizeof(double), w.E, n * sizeof(double), n * sizeof(double), n,
                           hipMemcpyDeviceToDevice, s));
   if ((rc = trsm_left(w.T, n, n, 0, X, n, ldl, w.tws, s))) return rc;
   for (int it = 0; it < iters; ++it) {
     // T = A X^T (X lower), E = X T
     if ((rc = rgemm(w, 0, 1, n, 1.0, A, lda, X, ldl, 0.0, w.T, n, VGPOSP_FULL, 0, 1, s))) return rc;
     if ((rc = rgemm(w, 0, 0, n, 1.0, X, ldl, w.T, n, 0.0, w.E, n, VGPOSP_FULL, 1, 0, s))) return rc;
-    if (it == iters - 1) VG_HIP(hipMemsetAsync(w.amax, 0, sizeof(unsigned long long), s));
+    if (it == iters - 1) VG_HIP(vg_memset(w.amax, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(refine_phi_kernel, dim3(1, (unsigned)n), dim3(256), 0, s, w.E, n, w.amax);
     VG_LAUNCH_CHECK();
     // X <- X - Phi X  (out of place through Y)
-    VG_HIP(hipMemcpy2DAsync(w.Y, n * sizeof(double), X, ldl * sizeof(double), n * sizeof(double),
+    VG_HIP(vg_memcpy2d(w.Y, n * sizeof(double), X, ldl * sizeof(double), n * sizeof(double),
                             n, hipMemcpyDeviceToDevice, s));
     if ((rc = rgemm(w, 0, 0, n, -1.0, w.E, n, w.Y, n, 1.0, X, ldl, VGPOSP_LOWER, 1, 1, s))) return rc;
   }

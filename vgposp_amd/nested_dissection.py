@@ -194,90 +194,37 @@ class FrontalTree:
                 raise AssertionError(f"front {i}: halo outside its ancestors")
 
     def _groups(self):
-        """Fronts of one depth form a level; a level is cut into groups of similar padded size
-        (every front of a group is padded to the group's (p, u)), largest u first, starting a new
-        group when u falls below (1 - tol) of the group's largest, so padding wastes little."""
-        tol = 0.1
-        bydepth = {}
-        for i, f in enumerate(self.fronts):
-            bydepth.setdefault(f.depth, []).append(i)
-        self.groups: list[Group] = []
-        self.levels = []            # per level: list of group indices, and total buffer sizes
-        for d in sorted(bydepth, reverse=True):          # deepest first = bottom-up order
-            ids = bydepth[d]
-            key = lambda i: (-_round_up(max(len(self.fronts[i].piv), 1), self.pad),
-                             -len(self.fronts[i].U), i)
-            ids = sorted(ids, key=key)
-            lvl = {"depth": d, "groups": [], "size": [0, 0, 0]}
-            cur = []
-            for i in ids:
-                if cur:
-                    f0 = self.fronts[cur[0]]
-                    f = self.fronts[i]
-                    same_p = (_round_up(max(len(f.piv), 1), self.pad)
-                              == _round_up(max(len(f0.piv), 1), self.pad))
-                    if not same_p or len(f.U) < (1 - tol) * len(f0.U):
-                        self._new_group(d, cur, lvl)
-                        cur = []
-                cur.append(i)
-            if cur:
-                self._new_group(d, cur, lvl)
-            self.levels.append(lvl)
-        for g in self.groups:
-            nf = g.nf
-            g.piv = np.full((nf, g.p), -1, dtype=np.int32)
-            g.U = np.full((nf, max(g.u, 1)), self.n, dtype=np.int32)
-            g.ulen = np.zeros(nf, dtype=np.int32)
-            g.pmap = np.full((nf, max(g.u, 1)), -1, dtype=np.int32)
-            g.parent_group = np.full(nf, -1, dtype=np.int32)
-            g.parent_slot = np.full(nf, -1, dtype=np.int32)
-            g.sibling = np.zeros(nf, dtype=np.int32)
-            g.order = np.asarray(g.fronts, dtype=np.int32)
-            g.par_off = np.full((nf, 3), -1, dtype=np.int64)
-            g.par_dim = np.full((nf, 2), -1, dtype=np.int32)
+        """The single-rank layout (every front on this process): ``self.groups`` / ``levels``."""
+        lay = FrontalLayout(self, world=1, rank=0)
+        self.groups, self.levels = lay.groups, lay.levels
+        for gi, g in enumerate(self.groups):
             for s, i in enumerate(g.fronts):
-                f = self.fronts[i]
-                g.piv[s, :len(f.piv)] = f.piv
-                g.U[s, :len(f.U)] = f.U
-                g.ulen[s] = len(f.U)
-                g.sibling[s] = f.sibling
-                if f.parent >= 0:
-                    par = self.fronts[f.parent]
-                    pg = self.groups[par.group]
-                    g.parent_group[s] = par.group
-                    g.parent_slot[s] = par.slot
-                    g.par_off[s] = (pg.off[0] + par.slot * pg.p * pg.p,
-                                    pg.off[1] + par.slot * pg.u * pg.p,
-                                    pg.off[2] + par.slot * pg.u * pg.u)
-                    g.par_dim[s] = (pg.p, pg.u)
-                    own = self.owner[f.U]
-                    pos = np.where(own == f.parent, self.owner_pos[f.U], -1)
-                    inU = own != f.parent
-                    k = np.searchsorted(par.U, f.U[inU])
-                    if np.any(k >= len(par.U)) or np.any(par.U[np.minimum(k, len(par.U) - 1)]
-                                                        != f.U[inU]):
-                        raise AssertionError("child boundary not inside the parent's front")
-                    pos[inU] = pg.p + k
-                    g.pmap[s, :len(f.U)] = pos
+                self.fronts[i].group = gi
+                self.fronts[i].slot = s
 
-    def _new_group(self, depth, ids, lvl):
-        gi = len(self.groups)
-        g = Group(depth, all(self.fronts[i].leaf for i in ids), list(ids))
-        g.p_max = max(len(self.fronts[i].piv) for i in ids)
-        g.u_max = max(len(self.fronts[i].U) for i in ids)
-        g.p = _round_up(max(g.p_max, 1), self.pad)
-        g.u = _round_up(g.u_max, self.pad) if g.u_max else 0
-        g.level = len(self.levels)
-        sz = lvl["size"]
-        g.off = (sz[0], sz[1], sz[2])
-        sz[0] += g.nf * g.p * g.p
-        sz[1] += g.nf * g.u * g.p
-        sz[2] += g.nf * g.u * g.u
-        for s, i in enumerate(ids):
-            self.fronts[i].group = gi
-            self.fronts[i].slot = s
-        self.groups.append(g)
-        lvl["groups"].append(gi)
+    def owners(self, world):
+        """Subtree-to-subcube mapping of the fronts onto `world` ranks: a front owning ranks
+        [lo, hi) gives its first child [lo, mid) and its second [mid, hi); the front itself runs on
+        rank lo.  With world = 2^d every front of depth >= d is private to one rank and the top
+        2^d - 1 fronts sit on the ranks that hold their first child's subtree."""
+        own = np.zeros(len(self.fronts), dtype=np.int64)
+        root = len(self.fronts) - 1
+
+        def go(i, lo, hi):
+            own[i] = lo
+            kids = self.fronts[i].children
+            if len(kids) == 2 and hi - lo > 1:
+                mid = (lo + hi + 1) // 2
+                go(kids[0], lo, mid)
+                go(kids[1], mid, hi)
+            else:
+                for c in kids:
+                    go(c, lo, hi)
+        go(root, 0, int(world))
+        return own
+
+    def layout(self, world=1, rank=0):
+        return FrontalLayout(self, world, rank)
 
     # ------------------------------------------------------------------ summaries
     def flops(self, padded=True):
@@ -320,4 +267,194 @@ def frontal_tree(shape, offsets, leaf=512, pad=16):
     return _cached(tuple(int(s) for s in shape), offs, int(leaf), int(pad))
 
 
-__all__ = ["FrontalTree", "Front", "Group", "frontal_tree", "stencil_radius"]
+
+
+class FrontalLayout:
+    """The fronts one rank factors, cut into levels (tree depths, deepest first) and groups of
+    similar padded size, each level stored as three flat buffers (PP, UP, UU) holding its groups at
+    static offsets.  A child whose parent is on the same rank addresses the parent front by its
+    offsets into the parent level's buffers (Group.par_off / par_dim); a child whose parent is on
+    another rank is a *transfer*: its update (factor phase) goes to the parent's rank as an
+    [ulen, ulen] block, and the parent's rank sends back that child's Q_UU (selected inverse).
+
+      send_update[li]  : (group, slot, front, dest) after level li is factored
+      recv_update[li]  : RemoteChild records extend-added into level li before it is factored
+      send_q[li]       : RemoteChild records gathered from level li's Q and sent after it
+      recv_q[li]       : (group, slot, front, src) whose Q_UU arrives before level li's selinv
+    """
+
+    tol = 0.1
+
+    def __init__(self, tree, world=1, rank=0):
+        self.tree = tree
+        self.world, self.rank = int(world), int(rank)
+        T = tree
+        self.owner = T.owners(world) if world > 1 else np.zeros(len(T.fronts), dtype=np.int64)
+        mine = [i for i in range(len(T.fronts)) if self.owner[i] == rank]
+        maxd = max(f.depth for f in T.fronts)
+        bydepth = {d: [] for d in range(maxd, -1, -1)}
+        for i in mine:
+            bydepth[T.fronts[i].depth].append(i)
+        self.groups: list[Group] = []
+        self.levels = []
+        self.where = {}          # front -> (group, slot)
+        self.depth_level = {}
+        for d in range(maxd, -1, -1):
+            ids = sorted(bydepth[d], key=lambda i: (-_round_up(max(len(T.fronts[i].piv), 1),
+                                                               T.pad), -len(T.fronts[i].U), i))
+            lvl = {"depth": d, "groups": [], "size": [0, 0, 0]}
+            self.depth_level[d] = len(self.levels)
+            self._cut(ids, d, lvl)
+            self.levels.append(lvl)
+        L = len(self.levels)
+        self.send_update = [[] for _ in range(L)]
+        self.recv_update = [[] for _ in range(L)]
+        self.send_q = [[] for _ in range(L)]
+        self.recv_q = [[] for _ in range(L)]
+        for gi, g in enumerate(self.groups):
+            self._fill(gi, g)
+        # children of this rank's fronts that live on other ranks
+        for i in mine:
+            for c in T.fronts[i].children:
+                if self.owner[c] != rank:
+                    rc = self._remote_child(c, i)
+                    li = self.depth_level[T.fronts[i].depth]
+                    self.recv_update[li].append(rc)
+                    self.send_q[li].append(rc)
+        for li in range(L):
+            self.recv_update[li].sort(key=lambda r: r.front)
+            self.send_q[li].sort(key=lambda r: r.front)
+            self.send_update[li].sort(key=lambda t: t[2])
+            self.recv_q[li].sort(key=lambda t: t[2])
+
+    def _cut(self, ids, d, lvl):
+        T = self.tree
+
+        def fl(p, u):
+            return p ** 3 + 3.0 * p * p * u + 3.0 * p * u * u
+
+        def dims(i):
+            f = T.fronts[i]
+            return (_round_up(max(len(f.piv), 1), T.pad), _round_up(len(f.U), T.pad))
+        cur = []
+        P = U = 0
+        worst = float("inf")
+        for i in ids:
+            pf, uf = dims(i)
+            if cur:
+                P2, U2, w2 = max(P, pf), max(U, uf), min(worst, fl(pf, uf))
+                if fl(P2, U2) > (1 + self.tol) * w2:
+                    self._new_group(d, cur, lvl)
+                    cur = []
+            if not cur:
+                P, U, worst = pf, uf, fl(pf, uf)
+            else:
+                P, U, worst = max(P, pf), max(U, uf), min(worst, fl(pf, uf))
+            cur.append(i)
+        if cur:
+            self._new_group(d, cur, lvl)
+
+    def _new_group(self, depth, ids, lvl):
+        T = self.tree
+        gi = len(self.groups)
+        g = Group(depth, all(T.fronts[i].leaf for i in ids), list(ids))
+        g.p_max = max(len(T.fronts[i].piv) for i in ids)
+        g.u_max = max(len(T.fronts[i].U) for i in ids)
+        g.p = _round_up(max(g.p_max, 1), T.pad)
+        g.u = _round_up(g.u_max, T.pad) if g.u_max else 0
+        g.level = len(self.levels)
+        sz = lvl["size"]
+        g.off = (sz[0], sz[1], sz[2])
+        sz[0] += g.nf * g.p * g.p
+        sz[1] += g.nf * g.u * g.p
+        sz[2] += g.nf * g.u * g.u
+        for s, i in enumerate(ids):
+            self.where[i] = (gi, s)
+        self.groups.append(g)
+        lvl["groups"].append(gi)
+
+    def _pmap(self, c, parent):
+        """Positions of child c's boundary in its parent's front (this rank's layout)."""
+        T = self.tree
+        f, par = T.fronts[c], T.fronts[parent]
+        pg = self.groups[self.where[parent][0]]
+        own = T.owner[f.U]
+        pos = np.where(own == parent, T.owner_pos[f.U], -1)
+        inU = own != parent
+        k = np.searchsorted(par.U, f.U[inU])
+        if np.any(k >= len(par.U)) or np.any(par.U[np.minimum(k, len(par.U) - 1)] != f.U[inU]):
+            raise AssertionError("child boundary not inside the parent's front")
+        pos[inU] = pg.p + k
+        return pos
+
+    def _par(self, parent):
+        pgi, ps = self.where[parent]
+        pg = self.groups[pgi]
+        return ((pg.off[0] + ps * pg.p * pg.p, pg.off[1] + ps * pg.u * pg.p,
+                 pg.off[2] + ps * pg.u * pg.u), (pg.p, pg.u))
+
+    def _fill(self, gi, g):
+        T = self.tree
+        nf = g.nf
+        g.piv = np.full((nf, g.p), -1, dtype=np.int32)
+        g.U = np.full((nf, max(g.u, 1)), T.n, dtype=np.int32)
+        g.ulen = np.zeros(nf, dtype=np.int32)
+        g.pmap = np.full((nf, max(g.u, 1)), -1, dtype=np.int32)
+        g.parent_group = np.full(nf, -1, dtype=np.int32)
+        g.parent_slot = np.full(nf, -1, dtype=np.int32)
+        g.sibling = np.zeros(nf, dtype=np.int32)
+        g.order = np.asarray(g.fronts, dtype=np.int32)
+        g.par_off = np.full((nf, 3), -1, dtype=np.int64)
+        g.par_dim = np.full((nf, 2), -1, dtype=np.int32)
+        li = g.level
+        for s, i in enumerate(g.fronts):
+            f = T.fronts[i]
+            g.piv[s, :len(f.piv)] = f.piv
+            g.U[s, :len(f.U)] = f.U
+            g.ulen[s] = len(f.U)
+            g.sibling[s] = f.sibling
+            if f.parent < 0:
+                continue
+            if self.owner[f.parent] != self.rank:
+                # the parent is elsewhere: sibling -1 keeps this front out of the local
+                # extend-add launches; its update and Q_UU travel as [ulen, ulen] blocks
+                g.sibling[s] = -1
+                self.send_update[li].append((gi, s, i, int(self.owner[f.parent])))
+                self.recv_q[li].append((gi, s, i, int(self.owner[f.parent])))
+                continue
+            pgi, ps = self.where[f.parent]
+            g.parent_group[s] = pgi
+            g.parent_slot[s] = ps
+            off, dim = self._par(f.parent)
+            g.par_off[s] = off
+            g.par_dim[s] = dim
+            g.pmap[s, :len(f.U)] = self._pmap(i, f.parent)
+
+    def _remote_child(self, c, parent):
+        T = self.tree
+        f = T.fronts[c]
+        off, dim = self._par(parent)
+        return RemoteChild(front=c, parent=parent, src=int(self.owner[c]), ulen=len(f.U),
+                           sibling=f.sibling, pmap=self._pmap(c, parent).astype(np.int32),
+                           par_off=np.asarray(off, dtype=np.int64),
+                           par_dim=np.asarray(dim, dtype=np.int32))
+
+    def flops(self):
+        return sum(g.nf * (float(g.p) ** 3 + 3.0 * g.p * g.p * g.u + 3.0 * g.p * g.u * g.u)
+                   for g in self.groups)
+
+
+@dataclass
+class RemoteChild:
+    front: int
+    parent: int
+    src: int
+    ulen: int
+    sibling: int
+    pmap: np.ndarray
+    par_off: np.ndarray
+    par_dim: np.ndarray
+
+
+__all__ = ["FrontalTree", "FrontalLayout", "RemoteChild", "Front", "Group", "frontal_tree",
+           "stencil_radius"]

@@ -211,11 +211,10 @@ class VGPTrainOp:
         sX.copy_(Xb)
         sy.copy_(yb)
         g.replay()
-        # Wait for the replay on the host before reading its status.  Measured on this ROCm
-        # build: without the explicit stream sync the 10th back-to-back replay of this graph read
-        # corrupted statuses (tools/repro_vgp2.py); with it, every replay is bit-identical to the
-        # eager step.  The step already synchronised once per run through the status check.
-        torch.cuda.current_stream().synchronize()
+        # stream-ordered status read (one host sync per step, inside check_info).  The captured
+        # step holds only kernel nodes: the library's fills / 2-D copies are kernels
+        # (common.h vg_memset / vg_memcpy2d), which removed the stale-status reads seen when
+        # memset / memcpy nodes were replayed back to back (commit 4d967c4's host sync).
         linalg.check_info(status)
         return loss.clone()
 

@@ -89,31 +89,153 @@ class TaperProblem:
         return int(min(400, math.ceil(math.log(tol / 2) / math.log(rho)) + 4))
 
 
+class HipFrontalOps:
+    """The device operations of the multifrontal selected inverse on libvgposp (frontal.hip):
+    flat fp64 level buffers are torch tensors, every call enqueues on the current stream."""
+
+    def __init__(self, prob: TaperProblem):
+        self.p = prob
+        self.dev = prob.device
+
+    # buffers
+    def zeros(self, n):
+        return torch.zeros(max(int(n), 1), dtype=torch.float64, device=self.dev)
+
+    def empty(self, n):
+        return torch.empty(max(int(n), 1), dtype=torch.float64, device=self.dev)
+
+    @staticmethod
+    def at(buf, off):
+        return None if buf is None else buf[int(off):]
+
+    def ints(self, a, dtype=np.int32):
+        return _dev(np.asarray(a, dtype=dtype), self.dev,
+                    torch.int64 if dtype == np.int64 else torch.int32)
+
+    @staticmethod
+    def block(buf, off, rows, ld, cols):
+        """[rows, cols] view of a row-major block with leading dimension ld at offset off."""
+        return buf[int(off): int(off) + rows * ld].view(rows, ld)[:, :cols]
+
+    # dense / sparse front steps
+    def assemble(self, tree, g, d, PP, UP):
+        pr = self.p
+        call("vgposp_front_assemble", *pr.taper_args(), _p(pr.offs), pr.m, _p(pr.tau),
+             pr.tau.numel(), _p(d["owner_ord"]), _p(d["owner_pos"]), _p(d["piv"]), g.p,
+             _p(d["U"]), g.u, _p(d["ulen"]), _p(d["order"]), g.nf, _p(PP), _p(UP), _stream())
+
+    def extend_add(self, UUc, uc, nfc, pmap, par_off, par_dim, sibl, sib, PP, UP, UU):
+        call("vgposp_front_extend_add", _p(UUc), uc, nfc, _p(pmap), _p(par_off), _p(par_dim),
+             _p(sibl), sib, _p(PP), _p(UP), _p(UU), _stream())
+
+    def factor(self, PP, UP, UU, p, u, nf):
+        info = torch.empty(nf, dtype=I32, device=self.dev)
+        ws = torch.empty(query("vgposp_front_factor_workspace_bytes", p, u, nf),
+                         dtype=torch.uint8, device=self.dev)
+        call("vgposp_front_factor", _p(PP), _p(UP), _p(UU), p, u, nf, _p(info), _p(ws), ws.numel(),
+             _stream())
+        return info
+
+    def gather(self, QPP, QUP, QUU, pmap, par_off, par_dim, nfc, uc, out):
+        call("vgposp_front_gather", _p(QPP), _p(QUP), _p(QUU), _p(pmap), _p(par_off),
+             _p(par_dim), nfc, uc, _p(out), _stream())
+
+    def selinv(self, M, W, QUU, p, u, nf, QPP, QUP):
+        call("vgposp_front_selinv", _p(M), _p(W), _p(QUU), p, u, nf, _p(QPP), _p(QUP), _stream())
+
+    def diag(self, QPP, p, nf, piv, out):
+        call("vgposp_front_diag", _p(QPP), p, nf, _p(piv), _p(out), _stream())
+
+    @staticmethod
+    def nonzero_info(info):
+        bad = torch.nonzero(info).flatten()
+        return (int(bad[0]), int(info[int(bad[0])])) if len(bad) else None
+
+
+class FrontComm:
+    """Point-to-point transfers of [ulen, ulen] blocks between the ranks of the subcube mapping
+    and the final sum of the diag(Q) slabs: RCCL over xGMI for device tensors with the ``nccl``
+    backend, host-staged with gloo."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.bytes = 0
+
+    def _staged(self, t):
+        return self.dist.get_backend(self.group) == "gloo" and t.device.type != "cpu"
+
+    def send(self, t, dst):
+        t = t.contiguous()
+        self.bytes += t.numel() * t.element_size()
+        if self._staged(t):
+            self.dist.send(t.cpu(), dst, group=self.group)
+        else:
+            self.dist.send(t, dst, group=self.group)
+
+    def recv(self, t, src):
+        if self._staged(t):
+            h = torch.empty(t.shape, dtype=t.dtype)
+            self.dist.recv(h, src, group=self.group)
+            t.copy_(h)
+        else:
+            self.dist.recv(t, src, group=self.group)
+
+    def allreduce(self, t):
+        if self._staged(t):
+            h = t.cpu()
+            self.dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+        else:
+            self.dist.all_reduce(t, group=self.group)
+
+
 class FrontalSelectedInverse:
     """diag((Sigma + eps I)^-1) of a TaperProblem through the nested-dissection plan: bottom-up
     multifrontal Cholesky (assembly, extend-add, batched partial factorization per tree level),
-    then the top-down selected inverse.  Every call only enqueues work on the current stream."""
+    then the top-down selected inverse.  Every call only enqueues work on the current stream.
 
-    def __init__(self, prob: TaperProblem, leaf=512):
+    Over R ranks (``comm`` with world R): subtree-to-subcube mapping (nested_dissection.
+    FrontalLayout) — each rank factors its own subtrees, a front whose parent lives on another
+    rank sends its [u, u] update there and receives its Q_UU back, and the diag(Q) slabs are
+    summed at the end (each node belongs to exactly one rank)."""
+
+    def __init__(self, prob: TaperProblem, leaf=512, comm=None, ops=None):
         self.p = prob
         t0 = time.perf_counter()
         self.tree = frontal_tree(prob.shape, prob.offs_np, leaf)
+        self.comm = comm
+        world = comm.world if comm is not None else 1
+        rank = comm.rank if comm is not None else 0
+        self.lay = self.tree.layout(world, rank) if world > 1 else self.tree.layout(1, 0)
         self.plan_s = time.perf_counter() - t0
-        dev = prob.device
+        self.ops = ops if ops is not None else HipFrontalOps(prob)
+        o = self.ops
         T = self.tree
-        self.owner_ord = _dev(T.owner, dev)
-        self.owner_pos = _dev(T.owner_pos, dev)
+        self.owner_ord = o.ints(T.owner)
+        self.owner_pos = o.ints(T.owner_pos)
         self.g = []
-        for g in T.groups:
+        for g in self.lay.groups:
             self.g.append({
-                "piv": _dev(g.piv, dev), "U": _dev(g.U, dev), "ulen": _dev(g.ulen, dev),
-                "pmap": _dev(g.pmap, dev), "par_off": _dev(g.par_off, dev, torch.int64),
-                "par_dim": _dev(g.par_dim, dev), "sib": _dev(g.sibling, dev),
-                "order": _dev(g.order, dev)})
+                "piv": o.ints(g.piv), "U": o.ints(g.U), "ulen": o.ints(g.ulen),
+                "pmap": o.ints(g.pmap), "par_off": o.ints(g.par_off, np.int64),
+                "par_dim": o.ints(g.par_dim), "sib": o.ints(g.sibling), "order": o.ints(g.order),
+                "owner_ord": self.owner_ord, "owner_pos": self.owner_pos})
+        self.remote = {}
+        for li in range(len(self.lay.levels)):
+            for rc in self.lay.recv_update[li]:
+                self.remote[rc.front] = {
+                    "pmap": o.ints(rc.pmap[None, :]), "par_off": o.ints(rc.par_off[None, :],
+                                                                          np.int64),
+                    "par_dim": o.ints(rc.par_dim[None, :]), "sib": o.ints([rc.sibling])}
         self.infos = []
 
     def flops(self):
-        return self.tree.flops(padded=True)
+        """Padded flops of this rank's fronts."""
+        return self.lay.flops()
 
     def run(self, out=None, timer=None):
         """-> qdiag [N] (device).  Cholesky status per group in ``self.infos`` (device).
@@ -122,83 +244,98 @@ class FrontalSelectedInverse:
         Storage is per tree level: three flat buffers (PP, UP, UU) holding the level's groups at
         their plan offsets; a child's parent is addressed by its static offsets into the parent
         level's buffers (nested_dissection.Group.par_off)."""
-        prob, T = self.p, self.tree
+        o, T, lay, comm = self.ops, self.tree, self.lay, self.comm
         tick = timer if timer is not None else (lambda tag: None)
-        dev = prob.device
-        f64 = torch.float64
-        G = T.groups
-        L = T.levels
+        G, L = lay.groups, lay.levels
         store = [None] * len(L)
         uu_prev = None
         self.infos = []
         tick(("start", -1))
         for li, lvl in enumerate(L):
             s0, s1, s2 = lvl["size"]
-            PP = torch.zeros(max(s0, 1), dtype=f64, device=dev)
-            UP = torch.zeros(max(s1, 1), dtype=f64, device=dev)
-            UU = torch.zeros(max(s2, 1), dtype=f64, device=dev)
+            PP, UP, UU = o.zeros(s0), o.zeros(s1), o.zeros(s2)
             for gi in lvl["groups"]:
-                g, d = G[gi], self.g[gi]
-                call("vgposp_front_assemble", *prob.taper_args(), _p(prob.offs), prob.m,
-                     _p(prob.tau), prob.tau.numel(), _p(self.owner_ord), _p(self.owner_pos),
-                     _p(d["piv"]), g.p, _p(d["U"]), g.u, _p(d["ulen"]), _p(d["order"]), g.nf,
-                     _p(PP[g.off[0]:]), _p(UP[g.off[1]:]), _stream())
+                g = G[gi]
+                o.assemble(T, g, self.g[gi], o.at(PP, g.off[0]), o.at(UP, g.off[1]))
             if li > 0:
                 for ci in L[li - 1]["groups"]:
                     c, cd = G[ci], self.g[ci]
                     if not c.u:
                         continue
                     for sib in (0, 1):
-                        call("vgposp_front_extend_add", _p(uu_prev[c.off[2]:]), c.u, c.nf,
-                             _p(cd["pmap"]), _p(cd["par_off"]), _p(cd["par_dim"]), _p(cd["sib"]),
-                             sib, _p(PP), _p(UP), _p(UU), _stream())
+                        o.extend_add(o.at(uu_prev, c.off[2]), c.u, c.nf, cd["pmap"],
+                                     cd["par_off"], cd["par_dim"], cd["sib"], sib, PP, UP, UU)
+            for rc in lay.recv_update[li]:          # updates of children on other ranks
+                buf = o.empty(rc.ulen * rc.ulen)
+                comm.recv(buf[:rc.ulen * rc.ulen], rc.src)
+                r = self.remote[rc.front]
+                o.extend_add(buf, rc.ulen, 1, r["pmap"], r["par_off"], r["par_dim"], r["sib"],
+                             rc.sibling, PP, UP, UU)
+                del buf
             uu_prev = None
             for gi in lvl["groups"]:
                 g = G[gi]
-                info = torch.empty(g.nf, dtype=I32, device=dev)
-                ws = torch.empty(query("vgposp_front_factor_workspace_bytes", g.p, g.u, g.nf),
-                                 dtype=torch.uint8, device=dev)
-                call("vgposp_front_factor", _p(PP[g.off[0]:]), _p(UP[g.off[1]:] if g.u else None),
-                     _p(UU[g.off[2]:] if g.u else None), g.p, g.u, g.nf, _p(info), _p(ws),
-                     ws.numel(), _stream())
-                del ws
-                self.infos.append(info)
+                self.infos.append(o.factor(o.at(PP, g.off[0]), o.at(UP, g.off[1]) if g.u else None,
+                                           o.at(UU, g.off[2]) if g.u else None, g.p, g.u, g.nf))
+            for gi, s, fi, dst in lay.send_update[li]:
+                g = G[gi]
+                n = T.fronts[fi].U.size
+                comm.send(o.block(UU, g.off[2] + s * g.u * g.u, n, g.u, n).contiguous().reshape(-1),
+                          dst)
             tick(("factor", li))
             store[li] = (PP, UP)
             uu_prev = UU
         del uu_prev
-        qdiag = out if out is not None else torch.empty(prob.n, dtype=f64, device=dev)
+        qdiag = out if out is not None else o.empty(T.n)
+        if comm is not None and comm.world > 1:
+            qdiag.zero_()
         Qpar = None
         for li in range(len(L) - 1, -1, -1):
             lvl = L[li]
             s0, s1, s2 = lvl["size"]
             M, W = store[li]
-            QPP = torch.empty(max(s0, 1), dtype=f64, device=dev)
-            QUP = torch.empty(max(s1, 1), dtype=f64, device=dev)
-            QUU = torch.empty(max(s2, 1), dtype=f64, device=dev)
+            QPP, QUP = o.empty(s0), o.empty(s1)
+            QUU = o.zeros(s2) if lay.recv_q[li] else o.empty(s2)
             for gi in lvl["groups"]:
                 g, d = G[gi], self.g[gi]
-                if g.u:
-                    call("vgposp_front_gather", _p(Qpar[0]), _p(Qpar[1]), _p(Qpar[2]),
-                         _p(d["pmap"]), _p(d["par_off"]), _p(d["par_dim"]), g.nf, g.u,
-                         _p(QUU[g.off[2]:]), _stream())
-                call("vgposp_front_selinv", _p(M[g.off[0]:]), _p(W[g.off[1]:] if g.u else None),
-                     _p(QUU[g.off[2]:] if g.u else None), g.p, g.u, g.nf, _p(QPP[g.off[0]:]),
-                     _p(QUP[g.off[1]:] if g.u else None), _stream())
-                call("vgposp_front_diag", _p(QPP[g.off[0]:]), g.p, g.nf, _p(d["piv"]), _p(qdiag),
-                     _stream())
+                if g.u and Qpar is not None:
+                    o.gather(Qpar[0], Qpar[1], Qpar[2], d["pmap"], d["par_off"], d["par_dim"],
+                             g.nf, g.u, o.at(QUU, g.off[2]))
+            # Q_UU of fronts whose parent is on another rank (after the gathers, which leave
+            # those slots zero)
+            for gi, s, fi, src in lay.recv_q[li]:
+                g = G[gi]
+                n = T.fronts[fi].U.size
+                buf = o.empty(n * n)
+                comm.recv(buf[:n * n], src)
+                o.block(QUU, g.off[2] + s * g.u * g.u, n, g.u, n).copy_(
+                    buf[:n * n].reshape(n, n))
+                del buf
+            for gi in lvl["groups"]:
+                g, d = G[gi], self.g[gi]
+                o.selinv(o.at(M, g.off[0]), o.at(W, g.off[1]) if g.u else None,
+                         o.at(QUU, g.off[2]) if g.u else None, g.p, g.u, g.nf,
+                         o.at(QPP, g.off[0]), o.at(QUP, g.off[1]) if g.u else None)
+                o.diag(o.at(QPP, g.off[0]), g.p, g.nf, d["piv"], qdiag)
+            for rc in lay.send_q[li]:               # Q_UU for children on other ranks
+                r = self.remote[rc.front]
+                buf = o.empty(rc.ulen * rc.ulen)
+                o.gather(QPP, QUP, QUU, r["pmap"], r["par_off"], r["par_dim"], 1, rc.ulen, buf)
+                comm.send(buf[:rc.ulen * rc.ulen], rc.src)
+                del buf
             store[li] = None
             del M, W
             Qpar = (QPP, QUP, QUU)
             tick(("selinv", li))
+        if comm is not None and comm.world > 1:
+            comm.allreduce(qdiag)
         return qdiag
 
     def check(self):
-        for gi, info in enumerate(self.infos):
-            bad = torch.nonzero(info).flatten()
-            if len(bad):
-                b = int(bad[0])
-                raise CholeskyError(int(info[b]), b)
+        for info in self.infos:
+            bad = self.ops.nonzero_info(info)
+            if bad is not None:
+                raise CholeskyError(bad[1], bad[0])
 
 
 class ExactWindowGreedy:
@@ -262,6 +399,8 @@ class ExactWindowGreedy:
         full = torch.zeros((self.kmax,) + self.p.shape, dtype=torch.float64, device=self.ws.device)
         for t in range(self.kmax):
             l0, l1, l2 = (int(v) for v in lo[t])
+            if not all(0 <= l <= s - b for l, s, b in zip((l0, l1, l2), self.p.shape, self.box)):
+                continue  # no column for this pick (the last one, or not placed)
             full[t, l0:l0 + b0, l1:l1 + b1, l2:l2 + b2] = cols[t]
         return full.view(self.kmax, -1)
 
@@ -276,10 +415,13 @@ class ExactTaperPlacement:
     """One C4 problem end to end: selected inverse + rounds (device-resident)."""
 
     def __init__(self, X, shape, k, cutoff, beta=4.0, kind="eq", amp=1.0, ls=1.0, diag_shift=0.0,
-                 jitter=TF_JITTER, threshold=TF_SMALL, leaf=512, device=None):
+                 jitter=TF_JITTER, threshold=TF_SMALL, leaf=512, device=None, group=None):
         self.prob = TaperProblem(X, shape, beta, kind, amp, ls, diag_shift, jitter, threshold,
                                  device)
-        self.sel = FrontalSelectedInverse(self.prob, leaf)
+        import torch.distributed as dist
+        comm = FrontComm(group) if dist.is_initialized() and dist.get_world_size(group) > 1 \
+            else None
+        self.sel = FrontalSelectedInverse(self.prob, leaf, comm=comm)
         self.greedy = ExactWindowGreedy(self.prob, k, cutoff)
         self.k = int(k)
         self.qdiag = torch.empty(self.prob.n, dtype=torch.float64, device=self.prob.device)
@@ -293,7 +435,7 @@ class ExactTaperPlacement:
 
 
 def tapered_placement_algorithm_3(X, k, COVER_spatial, cutoff, beta=4.0, kernel="eq", amp=1.0,
-                                  ls=1.0, diag_shift=0.0, snapshots=False, leaf=512):
+                                  ls=1.0, diag_shift=0.0, snapshots=False, leaf=512, group=None):
     """snippets_a3.sparse_placement_algorithm_3(cov_vv, k, COVER_spatial, cutoff) for the tapered
     covariance of the grid points X (C order, COVER_spatial = (I0, I1, I2)), exact, without the
     dense cov_vv.  -> (picks as a list of np.int64 in selection order, the pick deltas,
@@ -302,7 +444,8 @@ def tapered_placement_algorithm_3(X, k, COVER_spatial, cutoff, beta=4.0, kernel=
     N = shape[0] * shape[1] * shape[2]
     if len(X) != N:                                         # snippets_a3.py:51 tf.Assert
         raise ValueError(f"assertion failed: N = {len(X)} != prod(COVER_spatial) = {N}")
-    run = ExactTaperPlacement(X, shape, k, cutoff, beta, kernel, amp, ls, diag_shift, leaf=leaf)
+    run = ExactTaperPlacement(X, shape, k, cutoff, beta, kernel, amp, ls, diag_shift, leaf=leaf,
+                              group=group)
     snaps = [] if snapshots else None
     picks = run.run(snaps).cpu().numpy()
     run.check()
@@ -310,5 +453,5 @@ def tapered_placement_algorithm_3(X, k, COVER_spatial, cutoff, beta=4.0, kernel=
     return [np.int64(a) for a in picks], run.greedy.pick_delta[:k].cpu().numpy(), dci
 
 
-__all__ = ["TaperProblem", "FrontalSelectedInverse", "ExactWindowGreedy", "ExactTaperPlacement",
-           "tapered_placement_algorithm_3"]
+__all__ = ["TaperProblem", "HipFrontalOps", "FrontComm", "FrontalSelectedInverse",
+           "ExactWindowGreedy", "ExactTaperPlacement", "tapered_placement_algorithm_3"]
