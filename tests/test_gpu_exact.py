@@ -162,3 +162,19 @@ def test_exact_alg3_ranks_on_one_gpu(world):
     for r in range(world):
         assert out[r][0] == [int(a) for a in A1]
         np.testing.assert_allclose(out[r][1], d1, rtol=1e-13)
+
+
+def test_exact_128cube_regression():
+    """Config C4 at full size (128^3, k = 50) reproduces the picks committed in
+    tests/golden/c4_picks.json (written by tools/bench_exact.py with PICKS_OUT; the same sequence
+    the 16^3-40^3 tests tie to the dense algorithm 3).  A regression pin, not a reference
+    fixture: no dense algorithm 3 fits 128^3."""
+    import json
+    import os
+    from vgposp_amd.sparse_placement import tapered_placement_algorithm_3
+    from vgposp_amd.workloads import c4_grid
+    with open(os.path.join(os.path.dirname(__file__), "golden", "c4_picks.json")) as f:
+        want = json.load(f)["picks"]
+    X, shape, ls = c4_grid()
+    A, _, _ = tapered_placement_algorithm_3(X, 50, shape, 3, 4.0, ls=ls, diag_shift=SHIFT)
+    assert [int(a) for a in A] == want

@@ -72,6 +72,10 @@ def main():
            "picks_head": [int(v) for v in picks[:8].cpu()],
            "prof": {kname: [round(v[0], 3), v[1]] for kname, v in prof.items()},
            "phases_ms": phases, "groups": run.sel.tree.summary()}
+    if os.environ.get("PICKS_OUT"):
+        with open(os.environ["PICKS_OUT"], "w") as f:
+            json.dump({"workload": f"c4_grid({n}) EQ ls 2h noise 1e-2+1e-6 beta 4 cutoff 3",
+                       "k": k, "picks": [int(v) for v in picks.cpu()]}, f)
     print(json.dumps(out), flush=True)
 
 
