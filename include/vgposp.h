@@ -333,17 +333,23 @@ int vgposp_greedy_step(const double* Sigma, int64_t n, int64_t lda, int kmax, in
  *   threshold   |nom| or |denom| < threshold -> delta = 0 (:480: 1e-7; 1e-8 for alg. 2)
  *   cache_init  initial lazy-cache value (:690: INF = 1e8; +inf for alg. 2)
  * vgposp_greedy_init(...) == vgposp_greedy_init_ex(..., 0, 1e-8, +inf, ...).
- * For n >= 8192 (and a stream not being captured) init synchronises the stream after the leading
- * half of every recursion node of order >= 8192 and returns 0 as soon as `info` is set: a
- * singular Sigma costs the factorization up to the failed pivot, not a whole factor + inverse,
- * before the caller's jitter retry (placement_algorithm2.py:399-413's pinv has no failure mode).
- * Sigma and the workspace are then undefined, as after any failed factorization.
+ * After a failed pivot every later launch of init's factorization and inverse reads `info` on
+ * the device and exits: a singular Sigma costs the factorization up to the failed pivot, not a
+ * whole factor + inverse, before the caller's jitter retry (placement_algorithm2.py:399-413's
+ * pinv has no failure mode) — without any host synchronisation, so init can be captured into a
+ * graph.  Sigma and the workspace are then undefined, as after any failed factorization.
  * vgposp_greedy_cache returns the device pointer of the lazy cache [n] (delta_cached): the
  * per-round snapshot delta_cached_iters[:, r] of the TF variant is a copy of it after round r. */
 int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int kmax, double jitter,
                           double threshold, double cache_init, int* info, void* ws,
                           size_t ws_bytes, void* stream);
 int vgposp_greedy_cache(void* ws, int64_t n, int kmax, double** cache);
+/* Mark candidate idx as never selectable (after init: it is never scored, never an arg-max,
+ * never counted in evals).  placement_algorithm2 factors an odd-order cov_vv as
+ * [Sigma 0; 0 s] at the even order n + 1 (the fast GEMM needs even leading dimensions; the leading
+ * block's factor and inverse are unchanged and the padding couples to nothing) and excludes the
+ * padding candidate with this. */
+int vgposp_greedy_exclude(void* ws, int64_t n, int kmax, int64_t idx, void* stream);
 
 /* Placement algorithm 3, the local-kernel greedy (snippets_a3.sparse_placement_algorithm_3,
  * snippets_a3.py:43-330; with vgposp_greedy_init_ex(..., 1e-6, 1e-7, 1e8, ...) as its tf_nominator

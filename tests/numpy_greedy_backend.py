@@ -29,6 +29,7 @@ class NumpyCholeskyOps:
         self.A = A
         self.n = A.shape[0]
         self.device = torch.device("cpu")
+        self.failed = False  # a leading minor was not positive definite (device `info` != 0)
 
     def split(self, n):
         return split_point(n)
@@ -36,7 +37,11 @@ class NumpyCholeskyOps:
     def block(self, col0, nb):
         s = slice(col0, col0 + nb)
         B = np.tril(self.A[s, s])
-        L = np.linalg.cholesky(B + np.tril(B, -1).T)
+        try:
+            L = np.linalg.cholesky(B + np.tril(B, -1).T)
+        except np.linalg.LinAlgError:
+            self.failed = True
+            L = np.eye(nb)
         low = np.tril(np.ones((nb, nb), dtype=bool))
         blk = self.A[s, s]
         blk[low] = L[low]
@@ -77,15 +82,24 @@ class NumpyCholeskyOps:
 
 
 class NumpyGreedyBackend:
-    def __init__(self, Sigma, kmax):
+    def __init__(self, Sigma, kmax, jitter=0.0):
         self.S = np.array(Sigma, dtype=np.float64)
         self.n = self.S.shape[0]
         self.kmax = kmax
+        self.eps = float(jitter)
         self._delta = torch.zeros(self.n, dtype=torch.float64)
         self._piv = torch.zeros(2 + 2 * kmax, dtype=torch.float64)
+        self.ok = True
+        self.L = None
 
     def init(self):
-        L = np.linalg.cholesky(self.S)
+        try:
+            L = np.linalg.cholesky(self.S + self.eps * np.eye(self.n))
+            self.ok = True
+        except np.linalg.LinAlgError:
+            L = np.eye(self.n)
+            self.ok = False
+        self.L = L
         self.M = np.linalg.inv(L)
         self.sdiag = np.diag(self.S).copy()
         self.colsq = np.sum(self.M ** 2, axis=0)
@@ -102,16 +116,19 @@ class NumpyGreedyBackend:
         self.sel_delta = []
 
     def prepare(self):
-        self.F = self.S.copy()
+        self.F = self.S + self.eps * np.eye(self.n)
 
     def chol_ops(self):
-        return NumpyCholeskyOps(self.F)
+        self._ops = NumpyCholeskyOps(self.F)
+        return self._ops
 
     def finish_slab(self, c0, c1):
         """After DistCholesky on chol_ops(): the partitioned state from the shared factor."""
         L = np.tril(self.F)
         self.init()
-        self.M = np.linalg.inv(L)
+        self.ok = bool(not self._ops.failed and np.all(np.isfinite(L)) and np.all(np.diag(L) > 0))
+        self.L = L
+        self.M = np.linalg.inv(L) if self.ok else np.eye(self.n)
         self.colsq = np.sum(self.M ** 2, axis=0)
         self._mask_slab(c0, c1)
 
@@ -149,7 +166,8 @@ class NumpyGreedyBackend:
             s = self.S[idx, a].copy()
             s -= piv[2:2 + t1] @ self.W[:t1][:, idx]
             q -= piv[2 + t1:2 + 2 * t1] @ self.V[:t1][:, idx]
-            w = s / np.sqrt(piv[0]) if piv[0] > 0 else 0 * s
+            noma = piv[0] + self.eps
+            w = s / np.sqrt(noma) if noma > 0 else 0 * s
             v = q / np.sqrt(piv[1]) if piv[1] > 0 else 0 * q
             self.W[t1, idx] = w
             self.V[t1, idx] = v
@@ -159,7 +177,7 @@ class NumpyGreedyBackend:
         for i in idx:
             if self.sel[i]:
                 continue
-            den = 1.0 / self.prec[i]
+            den = 1.0 / self.prec[i] - self.eps
             d[i] = 0.0 if (abs(den) < EPS or abs(self.nom[i]) < EPS) else self.nom[i] / den
 
     def select(self, rnd, lazy, c0, c1):
@@ -199,3 +217,18 @@ class NumpyGreedyBackend:
 
     def result(self):
         return [np.int64(s) for s in self.selected], np.array(self.sel_delta), None
+
+    # singular cov_vv (ShardedGreedyPlacement.run's jitter retry)
+    def factor_ok(self, c0, c1, partitioned, check_pivots):
+        if not self.ok:
+            return False
+        if not check_pivots:
+            return True
+        lii = np.diag(self.L)
+        return bool(np.min(lii * lii / self.sdiag) >= 100 * np.finfo(np.float64).eps * self.n)
+
+    def diag_scale(self):
+        return abs(float(np.mean(np.diag(self.S)))) or 1.0
+
+    def rejitter(self, eps):
+        self.__init__(self.S, self.kmax, jitter=eps)

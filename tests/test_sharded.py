@@ -171,3 +171,43 @@ def test_single_rank_numpy_backend_matches_oracle():
         e = CASES[name]
         sh = ShardedGreedyPlacement(NumpyGreedyBackend(placement_cov(name, e), e["k"]))
         assert [int(a) for a in sh.run(e["k"])[0]] == e["alg2"]
+
+
+def _singular_covs():
+    rng = np.random.default_rng(3)
+    X = rng.uniform(-1, 1, (48, 3))
+    X[7] = X[3]                                      # duplicated location
+    K = np.exp(-0.5 * ((X[:, None] - X[None]) ** 2).sum(-1) / 0.3 ** 2)
+    T = rng.normal(size=(40, 12))                    # 12 samples < 40 locations
+    return {"dup": K, "fewsamples": np.cov(T)}
+
+
+def _singular_worker(rank, world, port, partition, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.numpy_greedy_backend import NumpyGreedyBackend
+        from vgposp_amd.sharded_placement import ShardedGreedyPlacement
+        res = {}
+        for name, cov in _singular_covs().items():
+            sh = ShardedGreedyPlacement(NumpyGreedyBackend(cov, 6), partition_inverse=partition,
+                                        align=4)
+            res[name] = [int(a) for a in sh.run(6)[0]]
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("partition", [False, True])
+def test_sharded_singular_cov_matches_pinv(partition):
+    """the sharded run takes the single-GPU jitter retry on a singular cov_vv (failed
+    factorization or rounding-level pivot), decided identically on both ranks, and picks what
+    the reference's pinv picks."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_singular_worker, args=(2, _free_port(), partition, out), nprocs=2, join=True)
+    for name, cov in _singular_covs().items():
+        exp = [int(a) for a in op.placement_algorithm_2(cov, 6)]
+        for r in range(2):
+            assert out[r][name] == exp, (r, name)

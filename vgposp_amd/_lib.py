@@ -118,6 +118,7 @@ SIGNATURES = {
     "vgposp_greedy_init_ex": (_i32, [_c_void_p, _i64, _i64, _i32, _f64, _f64, _f64, _c_void_p,
                                      _c_void_p, _size, _c_void_p]),
     "vgposp_greedy_cache": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_c_void_p)]),
+    "vgposp_greedy_exclude": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p]),
     "vgposp_greedy_select_window": (_i32, [_i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _i64,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                            _c_void_p]),

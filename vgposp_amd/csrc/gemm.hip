@@ -51,7 +51,13 @@ struct GemmParams {
   // batch (grid.y of the fast kernel, grid.z of the reference kernel): element b reads
   // A + b sA, B + b sB and writes C + b sC (split-K partials at part + b sP)
   int64_t sA, sB, sC, sP;
+  // device abort flag (a failed pivot of the enclosing factorization): non-zero -> the launch
+  // does nothing (vgposp_greedy_init's early stop without a host synchronisation)
+  const int* abort;
 };
+
+// Set by a factorization for the GEMMs it launches from this thread (gemm_abort_scope).
+thread_local const int* tl_gemm_abort = nullptr;
 
 // Stage one operand tile (128 rows of the M/N dimension x 16 of K) into registers.
 //   KC: stored[row][k] (row = M/N index), MC: stored[k][row].
@@ -130,6 +136,7 @@ __device__ __forceinline__ double frag(const double* lds, int row, int k) {
 // TA: A stored k x m (A^T used).  TB: B stored n x k (B^T used).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_ref_kernel(GemmParams p, int vec_a, int vec_b) {
+  if (p.abort != nullptr && *p.abort != 0) return;
   constexpr bool A_KC = !TA;  // A[m][k] is k-contiguous
   constexpr bool B_KC = TB;   // B[n][k] is k-contiguous
   __shared__ double smem[2 * 2 * TILE_ELEMS];  // [buf][A|B][tile]
@@ -304,6 +311,7 @@ template <int CFG> struct GemmCfg {
 template <bool TA, bool TB, bool TRIA, bool TRIB, int CFG>
 __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm_glds_kernel(
     GemmParams p, int tiles_m, int tiles_n) {
+  if (p.abort != nullptr && *p.abort != 0) return;
   constexpr bool A_KC = !TA;
   constexpr bool B_KC = TB;
   constexpr int NSUB = GemmCfg<CFG>::NSUB, NW = GemmCfg<CFG>::NW, FI = GemmCfg<CFG>::FI;
@@ -685,7 +693,7 @@ int gemm_launch_batched(int transa, int transb, int64_t m, int64_t n, int64_t k,
     return 0;
   }
   GemmParams p{m, n, k, alpha, beta, A, lda, B, ldb, C, ldc, uplo_c, tri_a, tri_b, 1, 0, 0, nullptr,
-               sA, sB, sC, sP};
+               sA, sB, sC, sP, tl_gemm_abort};
   const int va = aligned16(A, lda) && (batch == 1 || sA % 2 == 0);
   const int vb = aligned16(B, ldb) && (batch == 1 || sB % 2 == 0);
   const bool even = (m % 2 == 0) && (n % 2 == 0) && (k % 2 == 0) && k > 0;
@@ -758,6 +766,8 @@ static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa =
   s = std::min<int64_t>(s, deep >= 8 ? deep : std::min<int64_t>(8, k / 64));
   return (int)std::max<int64_t>(s, 1);
 }
+
+void gemm_set_abort(const int* flag) { tl_gemm_abort = flag; }
 
 int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa) {
   return auto_splits(m, n, k, uplo_c, transa);

@@ -471,17 +471,12 @@ extern "C" int vgposp_greedy_init_ex(double* Sigma, int64_t n, int64_t lda, int 
   hipLaunchKernelGGL(greedy_init_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, Sigma,
                      n, lda, jitter, threshold, cache_init, w);
   VG_LAUNCH_CHECK();
-  // early: a failed pivot (a singular cov_vv) ends the factorization where it is found, so the
-  // host's jitter retry does not pay for a whole O(n^3) factorization + inverse first
+  // early: after a failed pivot (a singular cov_vv) every later launch of the factorization and
+  // inverse reads `info` on the device and exits, so the host's jitter retry does not pay for a
+  // whole O(n^3) factorization + inverse first — and nothing here synchronises the host
   int rc = potrf_one(Sigma, n, lda, /*invert=*/1, nullptr, info, greedy_fact_ws(ws, w, n), s,
                      /*early=*/true);
   if (rc) return rc;
-  if (n >= 8192) {  // potrf_one already synchronised: skip the rest after a failed pivot
-    int h = 0;
-    VG_HIP(hipMemcpyAsync(&h, info, sizeof(int), hipMemcpyDeviceToHost, s));
-    VG_HIP(hipStreamSynchronize(s));
-    if (h != 0) return 0;
-  }
   // Q_ii = |M e_i|^2 -> part (reduced in the round-0 update)
   dim3 g((unsigned)ceil_div(n, TRMV_COLS), (unsigned)ceil_div(n, RC));
   const int vec = (reinterpret_cast<uintptr_t>(Sigma) % 16 == 0) && (lda % 2 == 0);
@@ -787,5 +782,22 @@ extern "C" int vgposp_greedy_cache(void* ws, int64_t n, int kmax, double** cache
   VG_CHECK_ARG(kmax >= 1, 3);
   VG_CHECK_ARG(cache != nullptr, 4);
   *cache = greedy_layout(ws, n, kmax).cache;
+  return 0;
+}
+
+namespace vgposp {
+__global__ void greedy_exclude_kernel(unsigned char* selmask, int64_t idx) { selmask[idx] = 1; }
+}  // namespace vgposp
+
+extern "C" int vgposp_greedy_exclude(void* ws, int64_t n, int kmax, int64_t idx, void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(ws != nullptr, 1);
+  VG_CHECK_ARG(n >= 1, 2);
+  VG_CHECK_ARG(kmax >= 1, 3);
+  VG_CHECK_ARG(idx >= 0 && idx < n, 4);
+  GreedyWS w = greedy_layout(ws, n, kmax);
+  hipLaunchKernelGGL(greedy_exclude_kernel, dim3(1), dim3(1), 0, as_stream(stream), w.selmask, idx);
+  VG_LAUNCH_CHECK();
   return 0;
 }

@@ -25,6 +25,7 @@ int gemm_launch_split(int transa, int transb, int64_t m, int64_t n, int64_t k, d
                       double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int nsplit,
                       double* part, hipStream_t stream);
 int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa);
+void gemm_set_abort(const int* flag);
 int gemm_launch_batched(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
                         const double* A, int64_t lda, int64_t sA, const double* B, int64_t ldb,
                         int64_t sB, double beta, double* C, int64_t ldc, int64_t sC, int uplo_c,
@@ -133,7 +134,9 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
                                                                   double* linv, double* diag_out,
                                                                   int* info, int64_t stride_a,
                                                                   int64_t stride_linv = NB * NB,
-                                                                  int64_t stride_diag = -1) {
+                                                                  int64_t stride_diag = -1,
+                                                                  const int* abort = nullptr) {
+  if (abort != nullptr && *abort != 0) return;  // an earlier pivot failed (early mode)
   extern __shared__ double L[];  // [NB][LP2]
   __shared__ double rdiag[NB];
   __shared__ double XD[(NB / LW) * LW * LW];  // dense diagonal blocks of L^-1
@@ -335,8 +338,8 @@ struct Fact {
   int batch = 1;
   int64_t sA = 0, sW = 0;
   const double* ws0 = nullptr;
-  // stop early on a failed pivot: read `info` back after each large node's leading half (a
-  // stream sync per node of order >= EARLY_MIN) and abandon the rest of the factorization
+  // stop early on a failed pivot: every later leaf / GEMM launch reads `info` on the device and
+  // exits once it is set (no host synchronisation)
   bool early = false;
   double* leaf(int64_t col0) const { return linv_all + (col0 / NB) * NB * NB; }
   double* xblk(int64_t col0) const { return xinv + col0 * NBI; }
@@ -394,7 +397,7 @@ static int leaf_factor(const Fact& f, double* A, int jb, int64_t col0, int inver
   hipLaunchKernelGGL(potrf_leaf_kernel, dim3((unsigned)f.batch), dim3(LEAF_THREADS), leaf_shmem(),
                      f.s, A, f.lda, jb, col0, invert, f.leaf(col0),
                      f.diag_out ? f.diag_out + col0 : nullptr, f.info, f.sA, f.sW,
-                     f.batch > 1 ? f.diag_n : (int64_t)-1);
+                     f.batch > 1 ? f.diag_n : (int64_t)-1, f.early ? f.info : nullptr);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -453,18 +456,14 @@ static int trtri_rec(const Fact& f, double* A, int64_t lda, int64_t n, int64_t c
   return pgemm(f, 0, 0, n2, n1, n2, -1.0, A22, lda, f.work, n1, 0.0, A21, lda, VGPOSP_FULL, 1, 0);
 }
 
-// Early stop (Fact::early): nodes of at least this order check `info` after their leading half.
-// A failed pivot at column j then costs about the factorization of the leading j columns plus
-// one node's panel, instead of the whole O(n^3) recursion and inverse.
-constexpr int64_t EARLY_MIN = 8192;
-constexpr int POTRF_STOPPED = 1;  // internal: info != 0, the rest of the recursion was skipped
-
-static int early_stop(const Fact& f) {
-  int h = 0;
-  VG_HIP(hipMemcpyAsync(&h, f.info, sizeof(int), hipMemcpyDeviceToHost, f.s));
-  VG_HIP(hipStreamSynchronize(f.s));
-  return h != 0 ? POTRF_STOPPED : 0;
-}
+// Early stop (Fact::early): every leaf and GEMM launch of the recursion (and of the inverse after
+// it) first reads `info` on the device and does nothing once a pivot has failed, so a failed
+// factorization costs the work up to the failed pivot plus empty launches — with no host
+// synchronisation (the call only enqueues work and can be captured into a graph).
+struct AbortScope {
+  explicit AbortScope(const int* flag) { gemm_set_abort(flag); }
+  ~AbortScope() { gemm_set_abort(nullptr); }
+};
 
 // blocks: form the inverse of every NB < n <= NBI diagonal block (for trsm / trtri above it).
 static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0, bool blocks) {
@@ -476,7 +475,6 @@ static int potrf_rec(const Fact& f, double* A, int64_t n, int64_t col0, bool blo
   double* A22 = A21 + n1;
   const bool sub = blocks && !whole;  // inside a block the leaf-level path is used
   if ((rc = potrf_rec(f, A, n1, col0, sub))) return rc;
-  if (f.early && n >= EARLY_MIN && (rc = early_stop(f))) return rc;
   if ((rc = trsm_rec(f, A21, n2, f.lda, A, n1, col0, sub))) return rc;
   if ((rc = pgemm(f, 0, 1, n2, n2, n1, -1.0, A21, f.lda, A21, f.lda, 1.0, A22, f.lda,
                   VGPOSP_LOWER, 0, 0)))
@@ -564,16 +562,10 @@ int potrf_one(double* A, int64_t n, int64_t lda, int invert, double* diag_out, i
   if (int rc = ensure_leaf_attr()) return rc;
   const bool blocks = n > NBI;
   Fact f = make_fact(n, lda, ws, diag_out, info, stream);
-  if (early && n >= EARLY_MIN) {
-    // a stream being captured into a graph cannot be synchronised: no early stop there
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) == hipSuccess) f.early = cs == hipStreamCaptureStatusNone;
-    else (void)hipGetLastError();  // status unknown: keep the fully asynchronous path
-  }
+  f.early = early;
+  AbortScope scope(early ? info : nullptr);
   int rc = potrf_rec(f, A, n, 0, blocks);
-  if (rc == POTRF_STOPPED) return 0;  // info holds the failed leading minor
   if (rc || !invert) return rc;
-  if (f.early && (rc = early_stop(f))) return rc == POTRF_STOPPED ? 0 : rc;
   return trtri_rec(f, A, lda, n, 0, blocks);
 }
 

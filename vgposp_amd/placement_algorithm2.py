@@ -38,14 +38,26 @@ class GreedyPlacement:
     """
 
     def __init__(self, Sigma, kmax, copy=False, jitter=0.0, threshold=1e-8,
-                 cache_init=float("inf")):
+                 cache_init=float("inf"), pad_odd=False):
         S = linalg.as_device(Sigma)
         if S.dim() != 2 or S.shape[0] != S.shape[1]:
             raise ValueError("cov_vv must be a square matrix")
-        self.n = int(S.shape[0])
-        if not (1 <= kmax <= self.n):
-            raise ValueError(f"k must be in [1, {self.n}], got {kmax}")
-        self.S = S.clone() if copy else S
+        self.N = int(S.shape[0])                     # candidates
+        if not (1 <= kmax <= self.N):
+            raise ValueError(f"k must be in [1, {self.N}], got {kmax}")
+        # pad_odd (with copy): an odd order is factored as [Sigma 0; 0 s] at N + 1, so every
+        # recursion level runs on the fast (even-leading-dimension) GEMM; the padding candidate is
+        # excluded on device after init (vgposp_greedy_exclude) and couples to nothing
+        self.padded = bool(pad_odd and copy and self.N % 2 == 1 and self.N > 1)
+        if self.padded:
+            n = self.N
+            P = torch.zeros((n + 1, n + 1), dtype=torch.float64, device=S.device)
+            P[:n, :n].copy_(S)
+            P[n, n] = torch.diagonal(S).mean()
+            self.S = P
+        else:
+            self.S = S.clone() if copy else S
+        self.n = int(self.S.shape[0])                # the library's order
         self.kmax = int(kmax)
         dev = self.S.device
         self.ws = linalg.workspace(query("vgposp_greedy_workspace_bytes", self.n, self.kmax))
@@ -61,6 +73,8 @@ class GreedyPlacement:
     def init(self):
         call("vgposp_greedy_init_ex", _p(self.S), self.n, self.S.stride(0), self.kmax,
              *self.params, _p(self.info), _p(self.ws), self.ws.numel(), _stream())
+        if self.padded:
+            call("vgposp_greedy_exclude", _p(self.ws), self.n, self.kmax, self.N, _stream())
         self.rounds = 0
         return self
 
@@ -69,7 +83,7 @@ class GreedyPlacement:
         c = ctypes.c_void_p()
         call("vgposp_greedy_cache", _p(self.ws), self.n, self.kmax, ctypes.byref(c))
         off = c.value - self.ws.data_ptr()
-        return self.ws[off:off + 8 * self.n].view(torch.float64)
+        return self.ws[off:off + 8 * self.N].view(torch.float64)
 
     def check(self):
         linalg.check_info(self.info)
@@ -159,7 +173,7 @@ def _place(cov_vv, k, lazy, verbose, trace=None):
         trace = []
     tr = None if trace is None else []
     try:
-        g = GreedyPlacement(cov_vv, k, copy=True)
+        g = GreedyPlacement(cov_vv, k, copy=True, pad_odd=True)
         sdiag = torch.diagonal(g.S).clone()
         g.init()
         _check_pivots(g, sdiag)
@@ -170,7 +184,7 @@ def _place(cov_vv, k, lazy, verbose, trace=None):
         for rel in SINGULAR_EPS:
             try:
                 tr = None if trace is None else []
-                g = GreedyPlacement(S, k, copy=True, jitter=rel * scale).init()
+                g = GreedyPlacement(S, k, copy=True, jitter=rel * scale, pad_odd=True).init()
                 A = _rounds(g, k, lazy, tr)
                 break
             except CholeskyError:

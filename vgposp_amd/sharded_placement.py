@@ -68,9 +68,11 @@ def inverse_slabs(n, world, align=128):
 class HipGreedyBackend:
     """The per-rank device state: a GreedyPlacement plus tensor views of its delta / pivot."""
 
-    def __init__(self, Sigma, kmax, copy=False):
+    def __init__(self, Sigma, kmax, copy=False, jitter=0.0):
         from .placement_algorithm2 import GreedyPlacement
-        self.g = GreedyPlacement(Sigma, kmax, copy=copy)
+        self._src = Sigma if copy else None
+        self.g = GreedyPlacement(Sigma, kmax, copy=copy, jitter=jitter)
+        self.sdiag = torch.diagonal(self.g.S).clone()
         self.n = self.g.n
         self.kmax = self.g.kmax
         d, p, plen = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
@@ -87,6 +89,35 @@ class HipGreedyBackend:
 
     def init(self):
         self.g.init()
+
+    # singular cov_vv (placement_algorithm2._place's rules, decided identically on every rank:
+    # each holds the same factor)
+    def factor_ok(self, c0, c1, partitioned, check_pivots):
+        """No failed pivot, and (check_pivots) no pivot ratio L_ii^2 / sigma_ii at rounding level.
+        The factored buffer holds L^-1 in the columns this rank inverted (all of them unless
+        partitioned) and L elsewhere."""
+        from .placement_algorithm2 import PIVOT_RTOL
+        g = self.g
+        if int(g.info.item()) != 0:
+            return False
+        if not check_pivots:
+            return True
+        d = torch.diagonal(g.S).clone()
+        inv = torch.ones_like(d, dtype=torch.bool)
+        if partitioned:
+            inv.zero_()
+            inv[c0:c1] = True
+        lii = torch.where(inv, 1.0 / d, d)
+        return bool(torch.min(lii * lii / self.sdiag) >= PIVOT_RTOL * g.n)
+
+    def diag_scale(self):
+        return float(torch.mean(self.sdiag).abs()) or 1.0
+
+    def rejitter(self, eps):
+        """Start over on Sigma + eps I with denom = 1 / P_yy - eps (vgposp_greedy_init_ex)."""
+        if self._src is None:
+            raise RuntimeError("the jitter retry needs the backend to own a copy of Sigma")
+        self.__init__(self._src, self.kmax, copy=True, jitter=eps)
 
     def init_slab(self, c0, c1):
         """Factor Sigma, form L^-1 only in columns [c0, c1) (vgposp_greedy_init_slab)."""
@@ -207,7 +238,7 @@ class ShardedGreedyPlacement:
         else:
             dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group)
 
-    def run(self, k, lazy=True):
+    def _factor(self):
         if self.partition and self.world > 1 and self.dist_factor:
             from .dist_cholesky import DIST_MIN, DistCholesky
             self.b.prepare()
@@ -219,6 +250,23 @@ class ShardedGreedyPlacement:
             self.b.init_slab(self.c0, self.c1)
         else:
             self.b.init()
+
+    def run(self, k, lazy=True):
+        """snippets of placement_algorithm2.py:151-219 over the ranks.  A singular cov_vv takes
+        the single-GPU path's jitter retry (SINGULAR_EPS relative to the mean diagonal), decided
+        identically on every rank."""
+        from ._lib import CholeskyError
+        from .placement_algorithm2 import SINGULAR_EPS
+        self._factor()
+        if not self.b.factor_ok(self.c0, self.c1, self.partition, check_pivots=True):
+            scale = self.b.diag_scale()
+            for rel in SINGULAR_EPS:
+                self.b.rejitter(rel * scale)
+                self._factor()
+                if self.b.factor_ok(self.c0, self.c1, self.partition, check_pivots=False):
+                    break
+            else:
+                raise CholeskyError(1)
         for rnd in range(k):
             if self.partition and rnd > 0:
                 self.b.extract(rnd, self.c0, self.c1)

@@ -46,7 +46,7 @@ def sparse_placement_algorithm_2(cov_vv, k, COVER_spatial, jitter=TF_JITTER, thr
     if N != cover:
         raise ValueError(f"assertion failed: N = {N} != prod(COVER_spatial) = {cover}")
     g = GreedyPlacement(cov_vv, k, copy=True, jitter=jitter, threshold=threshold,
-                        cache_init=cache_init)
+                        cache_init=cache_init, pad_odd=True)
     g.init()
     cache = g.cache()
     dci = torch.empty((k, N), dtype=torch.float64, device=cache.device)
