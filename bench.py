@@ -190,32 +190,55 @@ def load_traffic(path, kernel, N, shape, k):
     return {"bytes_per_launch": kern["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
 
 
-def vgp_line(args, which="c3", precision="fp64"):
-    """Config C3 or C5: VGP training steps/s on this GPU — optimal posterior over all
-    N + minibatch ELBO + analytic gradient + Adam(0.01), minibatch N / 8.
+def _committed(name, picks):
+    """Whether `picks` equal the selection committed in tests/golden/<name> (written from a
+    one-GPU run; at N > 1 the sharded path must reproduce it), None if absent."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", name)) as f:
+            want = json.load(f).get("picks")
+    except (OSError, ValueError):
+        return None
+    return None if want is None else [int(a) for a in picks] == [int(a) for a in want]
+
+
+def vgp_line(args, which="c3", precision="fp64", world=1, rank=0, barrier=None, maxtime=None):
+    """Config C3 or C5: VGP training steps/s — optimal posterior over all N +
+    minibatch ELBO + analytic gradient + Adam(0.01), minibatch N / 8.
       C3: N = 64^3 observations over [-7, 7]^3, M = 8^3, 3-D.
-      C5: N = 65,536 uniform over [-2, 2]^5, M = 4^5 = 1,024, 5-D (computed in fp64, at or above
-          the fp32 + refinement the config names)."""
+      C5: N = 65,536 uniform over [-2, 2]^5, M = 4^5 = 1,024, 5-D (fp64, or the fp32 factor +
+          fp64 refinement the config names).
+    With world > 1 the N observations are sharded over the ranks (data parallel):
+    each rank assembles its Kzx slab and its share of Kzx Kzx^T / Kzx y, two all-reduces per step
+    (M^2 + M, then 2 + M d doubles), the same minibatch on every rank; strong scaling."""
     import torch
+    import torch.distributed as dist
 
     from vgposp_amd import _lib
     from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph, vgp_c5_data
     X, y, Z = vgp_c3_data() if which == "c3" else vgp_c5_data()
     N, M = len(X), len(Z)
     B = N // 8
-    train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B, precision=precision)
+    shard = np.array_split(np.arange(N), world)[rank]
+    group = dist.group.WORLD if world > 1 else None
+    kernel = "eq" if which == "c3" else "matern52"
+    train_op, loss, xb, yb = vgp_c3_graph(X[shard], y[shard], Z, B, precision=precision,
+                                          group=group, n_total=N, kernel=kernel)
     Xd = torch.as_tensor(X, device="cuda")
     yd = torch.as_tensor(y, device="cuda")
     rng = np.random.default_rng(1)
     idx = [torch.as_tensor(rng.integers(0, N, B), device="cuda") for _ in range(args.vgp_steps + 2)]
     first = float(train_op.run({xb: Xd[idx[0]], yb: yd[idx[0]]}))
-    train_op.run({xb: Xd[idx[1]], yb: yd[idx[1]]})  # captures the step's HIP graph
+    train_op.run({xb: Xd[idx[1]], yb: yd[idx[1]]})  # captures the step's HIP graph (1 rank)
     torch.cuda.synchronize()
+    if barrier:
+        barrier()
     t0 = time.perf_counter()
     for i in range(2, args.vgp_steps + 2):
         last = train_op.run({xb: Xd[idx[i]], yb: yd[idx[i]]})
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.vgp_steps
+    if barrier:
+        barrier()
+    dt = (maxtime(time.perf_counter() - t0) if maxtime else time.perf_counter() - t0) / args.vgp_steps
     # GEMM share from one more step run eagerly with the library's event timing on
     _lib.prof_enable(True)
     train_op.run({xb: Xd[idx[1]], yb: yd[idx[1]]})
@@ -226,14 +249,20 @@ def vgp_line(args, which="c3", precision="fp64"):
             "C5: 65,536 observations U[-2,2]^5, 4^5 inducing points, " +
             ("fp64" if precision == "fp64" else
              "M x M Cholesky in fp32 (f32 MFMA) + 3 fp64 refinement steps, the rest fp64"))
-    return {"metric": "VGP ELBO Adam steps/sec", "value": 1.0 / dt, "ms_per_step": dt * 1e3,
-            "config": {"workload": desc + ", EQ, optimal posterior over all N + minibatch ELBO + "
-                                          "grads + Adam(0.01)", "N": N, "M": M, "d": X.shape[1],
-                       "batch": B},
-            "loss_first": first, "loss_last": float(last),
-            "graph": bool(train_op.graph),
-            "gemm": {"ms_per_step": ms, "tflops": fl / (ms * 1e-3) / 1e12 if ms else None,
-                     "launches_per_step": n, "note": "one eager step with event timing"}}
+    out = {"metric": "VGP ELBO Adam steps/sec", "value": 1.0 / dt, "ms_per_step": dt * 1e3,
+           "n_gpus": world, "scaling": "strong" if world > 1 else None,
+           "config": {"workload": desc + (", EQ" if kernel == "eq" else ", MaternFiveHalves") +
+                                  ", optimal posterior over all N + minibatch ELBO + grads + "
+                                  "Adam(0.01)", "N": N, "M": M, "d": X.shape[1],
+                      "batch": B,
+                      "parallelism": "single" if world == 1 else f"observations sharded x{world}"},
+           "loss_first": first, "loss_last": float(last),
+           "graph": bool(train_op.graph),
+           "gemm": {"ms_per_step": ms, "tflops": fl / (ms * 1e-3) / 1e12 if ms else None,
+                    "launches_per_step": n, "note": "one eager step with event timing (rank 0)"}}
+    if world > 1:
+        out["allreduce_doubles_per_step"] = M * M + M + 2 + M * X.shape[1]
+    return out
 
 
 def c2_line(reps=5):
@@ -331,12 +360,6 @@ def c4_line(args, world, rank, barrier, maxtime):
     gms, gl, gfl, _ = prof.get("gemm_f64", (0.0, 0, 0.0, 0.0))
     gemm_tf = gfl / (gms * 1e-3) / 1e12 if gms else None
     picks = [int(v) for v in ref.cpu()]
-    expect = None
-    try:
-        with open(os.path.join(ROOT, "tests", "golden", "c4_picks.json")) as f:
-            expect = json.load(f)
-    except (OSError, ValueError):
-        pass
     return {"metric": "greedy sensor placements/sec", "value": k / dt, "unit": "placements/s",
             "ms_per_step": dt * 1e3, "n_gpus": world, "scaling": "strong",
             "config": {"workload": "C4: 128^3 jittered grid (N=2,097,152), EQ amp 1 ls 2h, "
@@ -348,7 +371,8 @@ def c4_line(args, world, rank, barrier, maxtime):
                        f"subtree-to-subcube selected inverse over {world} ranks, rounds replicated"},
             "picks_head": picks[:6],
             "deterministic_selection": same,
-            "matches_committed_picks": (picks == expect.get("picks")) if expect else None,
+            "matches_committed_picks": (_committed("c4_picks.json", picks)
+                                        if k == 50 and args.noise == 1e-2 else None),
             "selected_inverse": {
                 "ms": sel_ms, "flops_algorithmic": fl_alg, "flops_this_rank_padded": fl_rank,
                 "tflops_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12,
@@ -530,6 +554,11 @@ def main():
     torch.cuda.empty_cache()
 
     c4 = None if args.no_c4 else c4_line(args, world, rank, barrier, maxtime)
+    vgp = None
+    if not args.no_vgp:
+        kw = dict(world=world, rank=rank, barrier=barrier, maxtime=maxtime)
+        vgp = {"vgp_c3": vgp_line(args, "c3", **kw), "vgp_c5": vgp_line(args, "c5", **kw),
+               "vgp_c5_mixed": vgp_line(args, "c5", precision="mixed", **kw)}
     splits = splits_line(args, world, barrier, maxtime, rank) if world > 1 and not args.no_splits \
         else None
 
@@ -620,15 +649,17 @@ def main():
         "breakdown": breakdown,
         "deterministic_selection": deterministic,
         "selected_head": sel[:8],
+        "selected": sel,
+        "matches_committed_picks": (_committed("bench65k_picks.json", sel)
+                                    if (shape == (64, 32, 32) and k == 50 and args.kernel == "eq"
+                                        and args.noise == 1e-2) else None),
     }
     if c4 is not None:
         out["c4"] = c4
     if splits is not None:
         out["independent_splits"] = splits
-    if world == 1 and not args.no_vgp:
-        out["vgp_c3"] = vgp_line(args, "c3")
-        out["vgp_c5"] = vgp_line(args, "c5")
-        out["vgp_c5_mixed"] = vgp_line(args, "c5", precision="mixed")
+    if vgp is not None:
+        out.update(vgp)
     if world == 1 and not args.no_c2:
         out["c2"] = c2_line()
     if world == 1 and not args.no_cpu:

@@ -142,6 +142,20 @@ class TorchCpuFrontalOps:
                 if j >= 0:
                     o[j] = q[s * p * p + k * p + k]
 
+    def pack_lower(self, buf, off, ld, n):
+        A = buf[int(off): int(off) + n * ld].view(n, ld)[:, :n].numpy()
+        return torch.from_numpy(A[np.tril_indices(n)].copy())
+
+    def unpack_lower(self, packed, buf, off, ld, n, symmetric):
+        A = buf[int(off): int(off) + n * ld].view(n, ld)[:, :n].numpy()
+        A[np.tril_indices(n)] = packed.numpy()
+        if symmetric:
+            iu = np.triu_indices(n, 1)
+            A[iu] = A.T[iu]
+
+    def empty_packed(self, n):
+        return torch.zeros(n * (n + 1) // 2, dtype=torch.float64)
+
     @staticmethod
     def nonzero_info(info):
         bad = np.nonzero(info)[0]

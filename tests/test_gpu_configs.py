@@ -62,7 +62,7 @@ def test_c2_assembly_and_potrf():
     torch.cuda.empty_cache()
 
 
-def _vgp_case(which, precision="fp64"):
+def _vgp_case(which, precision="fp64", kind="eq"):
     from vgposp_amd import linalg
     from vgposp_amd.vgp_training import VGPObjective
     from vgposp_amd.workloads import vgp_c3_data, vgp_c5_data
@@ -72,12 +72,12 @@ def _vgp_case(which, precision="fp64"):
     B = N // 8
     bi = np.random.default_rng(3).integers(0, N, B)
     a, l, s = _sp(0.54), 1e-5 + _sp(0.54), _sp(0.54)
-    obj = VGPObjective("eq", X, y, precision=precision)
+    obj = VGPObjective(kind, X, y, precision=precision)
     dev = lambda v: torch.tensor(v, dtype=torch.float64, device="cuda")  # noqa: E731
     E, ga, gl, gs, gZ = obj.loss_and_grads(linalg.as_device(Z), dev(a), dev(l), dev(s),
                                            linalg.as_device(X[bi]), linalg.as_device(y[bi]), B / N)
     got = (float(E), float(ga), float(gl), float(gs), gZ.cpu().numpy())
-    ref = ogp.vgp_training_loss_grads("eq", Z, X, y, X[bi], y[bi], a, l, s, B / N)
+    ref = ogp.vgp_training_loss_grads(kind, Z, X, y, X[bi], y[bi], a, l, s, B / N)
     assert got[0] == pytest.approx(ref[0], rel=1e-8)
     scale = max(abs(ref[1]), abs(ref[2]), abs(ref[3]), float(np.abs(ref[4]).max()))
     for g, r in zip(got[1:4], ref[1:4]):
@@ -92,15 +92,19 @@ def test_c3_vgp_loss_and_grads_vs_oracle():
 
 
 @pytest.mark.timeout(400)
-def test_c5_vgp_loss_and_grads_vs_oracle():
-    _vgp_case("c5")
+@pytest.mark.parametrize("kind", ["eq", "matern52"])
+def test_c5_vgp_loss_and_grads_vs_oracle(kind):
+    """C5 with the arch-2 VGP's MaternFiveHalves (main_architecture_2_sampledistribution.py:211)
+    and with EQ."""
+    _vgp_case("c5", kind=kind)
 
 
 @pytest.mark.timeout(400)
-def test_c5_vgp_mixed_precision_vs_oracle():
+@pytest.mark.parametrize("kind", ["eq", "matern52"])
+def test_c5_vgp_mixed_precision_vs_oracle(kind):
     """C5 as named: the M x M factorizations in fp32 + fp64 refinement (vgposp_potrf_mixed).  ELBO
     and gradients within the fp64 tolerances of the oracle (north_star asks 1e-5 relative)."""
-    _vgp_case("c5", precision="mixed")
+    _vgp_case("c5", precision="mixed", kind=kind)
 
 
 @pytest.mark.timeout(400)

@@ -156,29 +156,44 @@ __global__ __launch_bounds__(256) void front_extend_add_kernel(
 }
 
 // Child's full Q_UU [uc][uc] <- its parent's Q front at (pmap[a], pmap[b]); 0 on padding.
+// Q_UU is symmetric: one workgroup per 64 x 64 tile pair on or below the diagonal reads the lower
+// tile once and writes it and its mirror (transposed through LDS), so both stores are coalesced.
 __global__ __launch_bounds__(256) void front_gather_kernel(
     const double* __restrict__ QPP, const double* __restrict__ QUP, const double* __restrict__ QUU,
     const int* __restrict__ pmap, const long long* __restrict__ par_off,
     const int* __restrict__ par_dim, int uc, double* __restrict__ out) {
+  __shared__ double tile[XT][XT + 1];
   const int s = blockIdx.z;
-  const int b = blockIdx.x * XT + (threadIdx.x & (XT - 1));
-  if (b >= uc) return;
+  const int bx = blockIdx.x, by = blockIdx.y;
+  if (bx > by) return;
+  const int tx = threadIdx.x & (XT - 1), ty = threadIdx.x >> 6;
   const int* m = pmap + (size_t)s * uc;
-  const int mb = m[b];
   const int p = par_dim[2 * s], u = par_dim[2 * s + 1];
   const double* base[3] = {QPP + par_off[3 * s], QUP + par_off[3 * s + 1],
                            QUU + par_off[3 * s + 2]};
   double* dst = out + (size_t)s * uc * uc;
-  const int a1 = min(uc, (int)(blockIdx.y + 1) * XT);
-  for (int aa = blockIdx.y * XT + (threadIdx.x >> 6); aa < a1; aa += 4) {
-    const int ma = m[aa];
+  const int b = bx * XT + tx;
+  const int mb = b < uc ? m[b] : -1;
+  for (int i = ty; i < XT; i += 4) {
+    const int aa = by * XT + i;
     double v = 0.0;
-    if (ma >= 0 && mb >= 0) {
-      int blk;
-      const size_t off = front_off(max(ma, mb), min(ma, mb), p, u, blk);
-      v = base[blk][off];
+    if (aa < uc) {
+      const int ma = m[aa];
+      if (ma >= 0 && mb >= 0) {
+        int blk;
+        const size_t off = front_off(max(ma, mb), min(ma, mb), p, u, blk);
+        v = base[blk][off];
+      }
+      if (b < uc) dst[(size_t)aa * uc + b] = v;
     }
-    dst[(size_t)aa * uc + b] = v;
+    tile[i][tx] = v;
+  }
+  if (bx == by) return;
+  __syncthreads();
+  // mirror: rows bx * 64 + i, columns by * 64 + tx
+  for (int i = ty; i < XT; i += 4) {
+    const int r = bx * XT + i, c = by * XT + tx;
+    if (r < uc && c < uc) dst[(size_t)r * uc + c] = tile[tx][i];
   }
 }
 

@@ -151,6 +151,21 @@ class HipFrontalOps:
         bad = torch.nonzero(info).flatten()
         return (int(bad[0]), int(info[int(bad[0])])) if len(bad) else None
 
+    # transfers carry the lower triangle only (row-packed, n (n + 1) / 2 doubles)
+    def pack_lower(self, buf, off, ld, n):
+        out = torch.empty(max(n * (n + 1) // 2, 1), dtype=torch.float64, device=self.dev)
+        call("vgposp_pack_rows", _p(buf[int(off):]), ld, 0, n, 0, n, 1, _p(out), 0, _stream())
+        return out[:n * (n + 1) // 2]
+
+    def unpack_lower(self, packed, buf, off, ld, n, symmetric):
+        call("vgposp_pack_rows", _p(buf[int(off):]), ld, 0, n, 0, n, 1, _p(packed), 1, _stream())
+        if symmetric:
+            call("vgposp_sym_from_lower", _p(buf[int(off):]), n, ld, _stream())
+
+    def empty_packed(self, n):
+        return torch.empty(max(n * (n + 1) // 2, 1), dtype=torch.float64,
+                           device=self.dev)[:n * (n + 1) // 2]
+
 
 class FrontComm:
     """Point-to-point transfers of [ulen, ulen] blocks between the ranks of the subcube mapping
@@ -266,8 +281,12 @@ class FrontalSelectedInverse:
                         o.extend_add(o.at(uu_prev, c.off[2]), c.u, c.nf, cd["pmap"],
                                      cd["par_off"], cd["par_dim"], cd["sib"], sib, PP, UP, UU)
             for rc in lay.recv_update[li]:          # updates of children on other ranks
-                buf = o.empty(rc.ulen * rc.ulen)
-                comm.recv(buf[:rc.ulen * rc.ulen], rc.src)
+                n = rc.ulen
+                pk = o.empty_packed(n)
+                comm.recv(pk, rc.src)
+                buf = o.zeros(n * n)
+                o.unpack_lower(pk, buf, 0, n, n, False)
+                del pk
                 r = self.remote[rc.front]
                 o.extend_add(buf, rc.ulen, 1, r["pmap"], r["par_off"], r["par_dim"], r["sib"],
                              rc.sibling, PP, UP, UU)
@@ -280,8 +299,7 @@ class FrontalSelectedInverse:
             for gi, s, fi, dst in lay.send_update[li]:
                 g = G[gi]
                 n = T.fronts[fi].U.size
-                comm.send(o.block(UU, g.off[2] + s * g.u * g.u, n, g.u, n).contiguous().reshape(-1),
-                          dst)
+                comm.send(o.pack_lower(UU, g.off[2] + s * g.u * g.u, g.u, n), dst)
             tick(("factor", li))
             store[li] = (PP, UP)
             uu_prev = UU
@@ -306,11 +324,10 @@ class FrontalSelectedInverse:
             for gi, s, fi, src in lay.recv_q[li]:
                 g = G[gi]
                 n = T.fronts[fi].U.size
-                buf = o.empty(n * n)
-                comm.recv(buf[:n * n], src)
-                o.block(QUU, g.off[2] + s * g.u * g.u, n, g.u, n).copy_(
-                    buf[:n * n].reshape(n, n))
-                del buf
+                pk = o.empty_packed(n)
+                comm.recv(pk, src)
+                o.unpack_lower(pk, QUU, g.off[2] + s * g.u * g.u, g.u, n, True)
+                del pk
             for gi in lvl["groups"]:
                 g, d = G[gi], self.g[gi]
                 o.selinv(o.at(M, g.off[0]), o.at(W, g.off[1]) if g.u else None,
@@ -321,7 +338,7 @@ class FrontalSelectedInverse:
                 r = self.remote[rc.front]
                 buf = o.empty(rc.ulen * rc.ulen)
                 o.gather(QPP, QUP, QUU, r["pmap"], r["par_off"], r["par_dim"], 1, rc.ulen, buf)
-                comm.send(buf[:rc.ulen * rc.ulen], rc.src)
+                comm.send(o.pack_lower(buf, 0, rc.ulen, rc.ulen), rc.src)
                 del buf
             store[li] = None
             del M, W

@@ -62,16 +62,22 @@ def c4_grid(n=128, seed=0):
     return grid_points(shape, jitter=0.05, seed=seed), shape, 2.0 * grid_spacing(shape)
 
 
-def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64"):
+def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64", group=None, n_total=None, kernel="eq"):
     """The reference's training graph (variational_Gaussian_process_example.py:51-102) in this
-    package's API -> (train_op, loss, x_batch placeholder, y_batch placeholder)."""
+    package's API -> (train_op, loss, x_batch placeholder, y_batch placeholder).  ``group``: the
+    observations (X, y) are this rank's shard of ``n_total`` (data-parallel optimal posterior,
+    two all-reduces per step); every rank feeds the same minibatch."""
     from . import distributions as tfd
     from . import psd_kernels as tfkern
     from .optimizers import AdamOptimizer
     from .variables import Softplus, Variable, placeholder
     amp = Softplus(Variable(0.54, name="amplitude"), offset=0.0)
     ls = Softplus(Variable(0.54, name="length_scale"), offset=1e-5)
-    kernel = tfkern.ExponentiatedQuadratic(amplitude=amp, length_scale=ls)
+    # C3 follows variational_Gaussian_process_example.py:55-57 (ExponentiatedQuadratic); C5 the
+    # arch-2 VGP's MaternFiveHalves (main_architecture_2_sampledistribution.py:211)
+    cls = {"eq": tfkern.ExponentiatedQuadratic, "matern52": tfkern.MaternFiveHalves,
+           "matern32": tfkern.MaternThreeHalves, "matern12": tfkern.MaternOneHalf}[kernel]
+    kernel = cls(amplitude=amp, length_scale=ls)
     noise = Softplus(Variable(0.54, name="observation_noise_variance"), offset=0.0)
     Zv = Variable(Z, name="inducing_index_points")
     loc, scale = tfd.VariationalGaussianProcess.optimal_variational_posterior(
@@ -84,5 +90,6 @@ def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64"):
     xb = placeholder(np.float64, [B, X.shape[1]], name="x_train_batch")
     yb = placeholder(np.float64, [B], name="y_train_batch")
     loss = vgp.variational_loss(observations=yb, observation_index_points=xb,
-                                kl_weight=float(B) / float(len(X)))
-    return AdamOptimizer(learning_rate=lr).minimize(loss, precision=precision), loss, xb, yb
+                                kl_weight=float(B) / float(n_total or len(X)))
+    return (AdamOptimizer(learning_rate=lr).minimize(loss, group=group, precision=precision), loss,
+            xb, yb)
