@@ -54,7 +54,9 @@ def parse():
     p.add_argument("--no-c2", action="store_true", help="skip the C2 assembly + potrf line")
     p.add_argument("--vgp-steps", type=int, default=10)
     p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 exact algorithm 3) line")
-    p.add_argument("--c4-steps", type=int, default=3)
+    p.add_argument("--c4-steps", type=int, default=10)
+    p.add_argument("--no-c4-selinv", action="store_true",
+                   help="skip the C4 selected-inverse cross-check run")
     p.add_argument("--no-splits", action="store_true",
                    help="skip the N > 1 independent-splits extra")
     p.add_argument("--backend", default="nccl",
@@ -312,11 +314,13 @@ def c2_line(reps=5):
 
 def c4_line(args, world, rank, barrier, maxtime):
     """Config C4: 128^3 = 2,097,152 candidates, k = 50, the reference's algorithm 3
-    (snippets_a3.py:43-364) on the beta = 4 tapered covariance, window cutoff 3 — exact: the
-    denominators over V \\ (A u {y}) from a nested-dissection multifrontal selected inverse
-    (fp64 MFMA fronts) plus one CG column per pick (vgposp_amd.sparse_placement).  One step = the
-    selected inverse + all k rounds (the symbolic plan depends only on the grid shape and the taper
-    support and is built once, outside the timed region, like an FFT plan; plan_s reports it)."""
+    (snippets_a3.py:43-364) on the beta = 4 tapered covariance, window cutoff 3, exact
+    (vgposp_amd.sparse_placement).  One step = the bounded-lazy form end to end: stencil
+    coefficients, upper bounds of every Q_yy from 8 CG steps per candidate (sharded over the
+    ranks, one all-gather), then the k rounds (refining a candidate by its CG column whenever the
+    arg-max lands on a bounded one; replicated on every rank).  The multifrontal selected inverse
+    (exact diag(Q) on fp64 MFMA fronts, subtree-to-subcube over the ranks) runs once beside it as
+    the cross-check of the picks and reports its own rate."""
     import torch
 
     from vgposp_amd import _lib
@@ -324,13 +328,11 @@ def c4_line(args, world, rank, barrier, maxtime):
     from vgposp_amd.workloads import c4_grid
     X, shape, ls = c4_grid()
     k, beta, cutoff = args.k, 4.0, 3
-    run = ExactTaperPlacement(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6)
+    run = ExactTaperPlacement(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6,
+                              method="bounds")
     run.run()
     torch.cuda.synchronize()
-    run.check()
     ref = run.greedy.picks[:k].clone()
-    comm = run.sel.comm
-    b0 = comm.bytes if comm is not None else 0
     reps = args.c4_steps
     barrier()
     torch.cuda.synchronize()
@@ -340,55 +342,99 @@ def c4_line(args, world, rank, barrier, maxtime):
     torch.cuda.synchronize()
     barrier()
     dt = maxtime(time.perf_counter() - t0) / reps
-    run.check()
-    exchanged = ((comm.bytes - b0) / reps) if comm is not None else 0
     same = bool(torch.equal(ref, run.greedy.picks[:k]))
+    picks = [int(v) for v in ref.cpu()]
+    # one profiled step: the bounds pass and the rounds separately
+    g = run.greedy
     _lib.prof_enable(True)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     barrier()
     ev[0].record()
-    run.sel.run(out=run.qdiag)
+    c0, c1 = (0, run.prob.n)
+    if world > 1:
+        from vgposp_amd.sparse_placement import slab_of
+        c0, c1 = slab_of(run.prob.n, world, rank)
+    K, scale, width = g.bound_qdiag(run.qdiag, c0, c1)
     ev[1].record()
-    run.greedy.run(run.qdiag, k)
+    if world > 1:
+        from vgposp_amd.sparse_placement import allgather_slabs
+        allgather_slabs(run.qdiag, run.group)
     ev[2].record()
+    g.run_bounded(run.qdiag, k)
+    ev[3].record()
     torch.cuda.synchronize()
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
-    sel_ms, rounds_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
-    fl_alg = run.sel.tree.flops(padded=False)
-    fl_rank = run.sel.flops()
-    gms, gl, gfl, _ = prof.get("gemm_f64", (0.0, 0, 0.0, 0.0))
-    gemm_tf = gfl / (gms * 1e-3) / 1e12 if gms else None
-    picks = [int(v) for v in ref.cpu()]
-    return {"metric": "greedy sensor placements/sec", "value": k / dt, "unit": "placements/s",
-            "ms_per_step": dt * 1e3, "n_gpus": world, "scaling": "strong",
-            "config": {"workload": "C4: 128^3 jittered grid (N=2,097,152), EQ amp 1 ls 2h, "
-                                   f"noise {args.noise}+1e-6, beta-decay taper beta={beta} "
-                                   f"(support {run.prob.m} points), window cutoff {cutoff}, k={k}, "
-                                   "exact algorithm 3 (dense-equivalent deltas, TF constants)",
-                       "N": int(np.prod(shape)), "k": k,
-                       "parallelism": "single" if world == 1 else
-                       f"subtree-to-subcube selected inverse over {world} ranks, rounds replicated"},
-            "picks_head": picks[:6],
-            "deterministic_selection": same,
-            "matches_committed_picks": (_committed("c4_picks.json", picks)
-                                        if k == 50 and args.noise == 1e-2 else None),
-            "selected_inverse": {
-                "ms": sel_ms, "flops_algorithmic": fl_alg, "flops_this_rank_padded": fl_rank,
-                "tflops_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12,
-                "mfma_frac_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
-                "gemm_tflops": gemm_tf,
-                "gemm_frac": gemm_tf / FP64_MFMA_PEAK_TFLOPS if gemm_tf else None,
-                "gemm_ms": gms, "gemm_launches": gl,
-                "fronts": len(run.sel.tree.fronts), "levels": len(run.sel.lay.levels),
-                "groups_this_rank": len(run.sel.lay.groups), "plan_s": run.sel.plan_s,
-                "exchanged_gb_per_step": exchanged / 1e9},
-            "rounds_ms": rounds_ms, "cg_iterations_per_pick": run.greedy.cg_iters,
-            "breakdown_ms": {n: v[0] for n, v in prof.items()},
-            "note": ("selected inverse = nested-dissection multifrontal Cholesky + Takahashi "
-                     "recurrences on batched fp64 MFMA fronts; per pick one CG column Q e_a (on the "
-                     "Krylov box of the pick) and a 216-candidate window re-score with |A| x |A| "
-                     "solves; the timing and rates above are rank 0's profiled step")}
+    bounds_ms, gather_ms, rounds_ms = (ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]),
+                                       ev[2].elapsed_time(ev[3]))
+    nb = c1 - c0
+    out = {"metric": "greedy sensor placements/sec", "value": k / dt, "unit": "placements/s",
+           "ms_per_step": dt * 1e3, "n_gpus": world, "scaling": "strong",
+           "config": {"workload": "C4: 128^3 jittered grid (N=2,097,152), EQ amp 1 ls 2h, "
+                                  f"noise {args.noise}+1e-6, beta-decay taper beta={beta} "
+                                  f"(support {run.prob.m} points), window cutoff {cutoff}, k={k}, "
+                                  "exact algorithm 3 (dense-equivalent deltas, TF constants)",
+                      "N": int(np.prod(shape)), "k": k,
+                      "parallelism": "single" if world == 1 else
+                      f"bounds sharded over {world} ranks (one all-gather), rounds replicated"},
+           "method": "bounded-lazy (K-step CG brackets of Q_yy, refinement by CG columns)",
+           "picks_head": picks[:6],
+           "deterministic_selection": same,
+           "matches_committed_picks": (_committed("c4_picks.json", picks)
+                                       if k == 50 and args.noise == 1e-2 else None),
+           "bounds": {"ms": bounds_ms, "cg_steps": K, "bracket_rel_width": width,
+                      "candidates_this_rank": nb,
+                      "mcandidates_per_s": nb / (bounds_ms * 1e-3) / 1e6},
+           "allgather_ms": gather_ms if world > 1 else None,
+           "exchanged_gb_per_step": (8.0 * (-(-run.prob.n // world)) * (world - 1) / 1e9
+                                     if world > 1 else 0.0),
+           "rounds_ms": rounds_ms, "refinements": g.refinements,
+           "cg_iterations_per_column": g.cg_iters,
+           "breakdown_ms": {n: v[0] for n, v in prof.items()}}
+    # the selected-inverse form once: the same picks, and the fp64-MFMA rate of its fronts
+    if not args.no_c4_selinv:
+        sel = ExactTaperPlacement(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6,
+                                  method="selinv")
+        sel.run()
+        torch.cuda.synchronize()
+        sel.check()
+        comm = sel.sel.comm
+        b0 = comm.bytes if comm is not None else 0
+        _lib.prof_enable(True)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        barrier()
+        e[0].record()
+        sel.sel.run(out=sel.qdiag)
+        e[1].record()
+        sel.greedy.run(sel.qdiag, k)
+        e[2].record()
+        torch.cuda.synchronize()
+        sprof = _lib.prof_dump()
+        _lib.prof_enable(False)
+        sel.check()
+        sel_ms = e[0].elapsed_time(e[1])
+        fl_alg = sel.sel.tree.flops(padded=False)
+        gms, gl, gfl, _ = sprof.get("gemm_f64", (0.0, 0, 0.0, 0.0))
+        gemm_tf = gfl / (gms * 1e-3) / 1e12 if gms else None
+        out["selected_inverse"] = {
+            "picks_equal": [int(v) for v in sel.greedy.picks[:k].cpu()] == picks,
+            "ms": sel_ms, "rounds_ms": e[1].elapsed_time(e[2]),
+            "placements_per_s": k / ((sel_ms + e[1].elapsed_time(e[2])) * 1e-3),
+            "flops_algorithmic": fl_alg, "flops_this_rank_padded": sel.sel.flops(),
+            "tflops_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12,
+            "mfma_frac_algorithmic": fl_alg / (sel_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "gemm_tflops": gemm_tf,
+            "gemm_frac": gemm_tf / FP64_MFMA_PEAK_TFLOPS if gemm_tf else None,
+            "gemm_ms": gms, "gemm_launches": gl,
+            "fronts": len(sel.sel.tree.fronts), "levels": len(sel.sel.lay.levels),
+            "groups_this_rank": len(sel.sel.lay.groups), "plan_s": sel.sel.plan_s,
+            "exchanged_gb": ((comm.bytes - b0) / 1e9) if comm is not None else 0.0,
+            "breakdown_ms": {n: v[0] for n, v in sprof.items()},
+            "note": "nested-dissection multifrontal Cholesky + Takahashi recurrences on batched "
+                    "fp64 MFMA fronts, then the plain rounds; one profiled run"}
+        del sel
+        torch.cuda.empty_cache()
+    return out
 
 
 def splits_line(args, world, barrier, maxtime, rank):

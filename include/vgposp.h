@@ -515,34 +515,65 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  * cutoff: the window [i_d - cutoff, i_d + cutoff) of snippets_a3.py:190-303; threshold: |nom| or
  * |denom| below -> delta 0, snippets_a2.py:480; radius: the stencil radius (largest offset
  * component); cg_iters: conjugate-gradient iterations per column).  qdiag [N]:
- * diag((Sigma + jitter I)^-1) from the front_* calls; cache [N] f64 (delta_cached), selected [N]
- * uint8, both caller-owned.
- *   vgposp_exact_prepare: the stencil coefficients, round 0 (every candidate: nom = s_yy,
- *     denom = 1 / Q_yy - jitter) and the arg-max keys; clears `selected`.
+ * diag((Sigma + jitter I)^-1) from the front_* calls, or upper bounds of it from
+ * vgposp_exact_bounds; cache [N] f64 (delta_cached), selected [N] uint8, both caller-owned.
+ *
+ * Selected-inverse form (qdiag exact):
+ *   vgposp_exact_prepare(flags = 0): the stencil coefficients, round 0 (every candidate:
+ *     nom = s_yy, denom = 1 / Q_yy - jitter) and the arg-max keys; clears `selected`.
  *   vgposp_exact_round:   pick `round` = the arg-max of the cache over V \ A (lowest index on ties),
  *     picks[round] / pick_delta[round]; unless `last`: q = Q e_pick by cg_iters CG iterations on
  *     Sigma + jitter I (stopping early once |r| <= cg_tol) on the box of half-width
  *     radius * cg_iters around the pick (the Krylov vectors are exactly zero beyond it), the next
  *     rows of chol(Q_AA) and chol(Sigma_AA + jitter I), and the window re-score
  *       nom = s_yy - |LS^-1 s_Ay|^2,  denom = 1 / (Q_yy - |LQ^-1 q_Ay|^2) - jitter.
- *   vgposp_exact_buffers: device addresses of the columns [kmax][b0 b1 b2] (box-local, C order,
- *     box dims b_d = min(2 radius cg_iters + 1, I_d)), their box origins int64 [kmax][3] and the
- *     CG state (int [2]: converged flag, iterations of the last solve). */
+ *
+ * Bounded-lazy form (no selected inverse; same picks):
+ *   vgposp_exact_coef:    the stencil coefficients and Gershgorin bounds [lambda_min, lambda_max]
+ *     of Sigma + jitter I (device doubles, vgposp_exact_buffers' `gersh`).
+ *   vgposp_exact_bounds:  qdiag[y] for y in [c0, c1) <- hi_scale * g_K(y), g_K = the K-step CG
+ *     estimate of e_y^T (Sigma + jitter I)^-1 e_y from x = 0 (a lower bound; hi_scale =
+ *     (1 + margin) / (1 - 4 rho^2K) makes it an upper bound).  tab_off int [T][3]: the offsets
+ *     within K stencil steps, sorted by step count (offset 0 first); tab_cnt int [K + 1]: offsets
+ *     within d steps; tab_nb int [T][m - 1]: row of (offset + offsets[o]) in the table or -1.
+ *     T <= 1024, T (m - 1) <= 8192.
+ *   vgposp_exact_prepare(flags = 1): round 0 from those bounds (cache = upper bounds).
+ *   vgposp_exact_argmax:  the arg-max candidate of the cache -> `cand` (vgposp_exact_buffers).
+ *   vgposp_exact_refine:  Q e_cand by CG into column slot `slot` (< 2 kmax); Q_cc becomes exact and
+ *     the candidate's cache entry the reference's value (scored with the A of its last re-score).
+ *   vgposp_exact_pick:    cand (refined, column in `slot`) becomes pick `round`.
+ *   vgposp_exact_update:  after pick `round`: the factor rows and the window re-score (upper
+ *     bounds where Q_yy is still only bounded).
+ *   The caller loops argmax -> (refine while the arg-max is not refined) -> pick -> update.
+ *
+ *   vgposp_exact_buffers: device addresses of the column slots [2 kmax][b0 b1 b2] (box-local, C
+ *     order, box dims b_d = min(2 radius cg_iters + 1, I_d)), their box origins int64
+ *     [2 kmax][3], the CG state (int [2]: converged flag, iterations of the last solve), the
+ *     column slot of every pick (int [kmax]), the arg-max candidate (int64) and the Gershgorin
+ *     bounds (double [2]). */
+#define VGPOSP_EXACT_ARGS                                                                         \
+  int kind, const double *X, int64_t I0, int64_t I1, int64_t I2, double amp, double ls,          \
+      double diag_shift, double jitter, double threshold, const int *offsets, int m,             \
+      const double *tau, int ntau, int kmax, int cutoff, int radius, int cg_iters,               \
+      const double *qdiag, double *cache, uint8_t *selected, void *ws, size_t ws_bytes
 size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
                                     int cg_iters);
-int vgposp_exact_prepare(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2, double amp,
-                         double ls, double diag_shift, double jitter, double threshold,
-                         const int* offsets, int m, const double* tau, int ntau, int kmax,
-                         int cutoff, int radius, int cg_iters, const double* qdiag, double* cache,
-                         uint8_t* selected, void* ws, size_t ws_bytes, void* stream);
-int vgposp_exact_round(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2, double amp,
-                       double ls, double diag_shift, double jitter, double threshold,
-                       const int* offsets, int m, const double* tau, int ntau, int kmax,
-                       int cutoff, int radius, int cg_iters, const double* qdiag, double* cache,
-                       uint8_t* selected, void* ws, size_t ws_bytes, int round, int last,
-                       int64_t* picks, double* pick_delta, double cg_tol, void* stream);
+int vgposp_exact_prepare(VGPOSP_EXACT_ARGS, int flags, void* stream);
+int vgposp_exact_round(VGPOSP_EXACT_ARGS, int round, int last, int64_t* picks, double* pick_delta,
+                       double cg_tol, void* stream);
+int vgposp_exact_coef(VGPOSP_EXACT_ARGS, void* stream);
+int vgposp_exact_bounds(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
+                        const int* tab_cnt, int T, int K, double hi_scale, int64_t c0, int64_t c1,
+                        void* stream);
+int vgposp_exact_argmax(VGPOSP_EXACT_ARGS, void* stream);
+int vgposp_exact_refine(VGPOSP_EXACT_ARGS, int slot, const int64_t* picks, double cg_tol,
+                        void* stream);
+int vgposp_exact_pick(VGPOSP_EXACT_ARGS, int round, int slot, int64_t* picks, double* pick_delta,
+                      void* stream);
+int vgposp_exact_update(VGPOSP_EXACT_ARGS, int round, const int64_t* picks, void* stream);
 int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
-                         int cg_iters, double** qcols, int64_t** boxlo, int** cgstate);
+                         int cg_iters, double** qcols, int64_t** boxlo, int** cgstate,
+                         int** slot_of_round, int64_t** cand, double** gersh);
 
 /* ---------------------------------------------------------------------------------------------
  * TF1 AdamOptimizer step on a device parameter vector (tf.train.AdamOptimizer in

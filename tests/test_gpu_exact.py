@@ -48,16 +48,17 @@ def test_selected_inverse_diag(shape, beta, leaf, kind):
     np.testing.assert_allclose(q, ref, rtol=1e-12)
 
 
-def test_cg_columns_match_dense_inverse():
+@pytest.mark.parametrize("method", ["selinv", "bounds"])
+def test_cg_columns_match_dense_inverse(method):
     from vgposp_amd.sparse_placement import ExactTaperPlacement
     shape = (12, 11, 10)
     X, ls = _grid(shape, seed=3)
-    run = ExactTaperPlacement(X, shape, 8, 3, ls=ls, diag_shift=SHIFT, leaf=128)
+    run = ExactTaperPlacement(X, shape, 8, 3, ls=ls, diag_shift=SHIFT, leaf=128, method=method)
     picks = run.run().cpu().numpy()
     C = _dense(X, shape, 4.0, ls) + 1e-6 * np.eye(len(X))
     Qinv = np.linalg.inv(C)
     cols = run.greedy.q_columns()
-    for t in range(7):  # the last pick has no column
+    for t in range(7 if method == "selinv" else 8):  # selinv: the last pick has no column
         np.testing.assert_allclose(cols[t].cpu().numpy(), Qinv[:, picks[t]], rtol=0,
                                    atol=1e-14 * Qinv[picks[t], picks[t]])
 
@@ -80,6 +81,74 @@ def test_exact_alg3_matches_oracle(shape, k, cutoff, beta, kind):
     assert [int(a) for a in A] == rA
     np.testing.assert_allclose(dci, rdci, rtol=1e-10, atol=1e-13)
     np.testing.assert_allclose(deltas, [rdci[a, i] for i, a in enumerate(rA)], rtol=1e-10)
+
+
+@pytest.mark.parametrize("shape,k,cutoff,beta,kind", [
+    ((8, 8, 8), 8, 3, 4.0, "eq"),
+    ((10, 9, 8), 10, 2, 4.0, "matern52"),
+    ((6, 7, 30), 12, 1, 4.0, "eq"),
+    ((14, 13, 12), 30, 3, 4.0, "matern32"),
+    ((20, 4, 9), 25, 2, 4.0, "matern12"),
+])
+def test_bounded_alg3_matches_oracle(shape, k, cutoff, beta, kind):
+    """The bounded-lazy rounds (upper bounds of Q_yy from K-step CG, refinement by the CG column
+    whenever the arg-max lands on a bounded candidate) pick the oracle's sensors with the
+    oracle's pick deltas."""
+    from vgposp_amd.sparse_placement import ExactTaperPlacement
+    X, ls = _grid(shape, seed=shape[0] * 7 + k)
+    run = ExactTaperPlacement(X, shape, k, cutoff, beta, kind, ls=ls, diag_shift=SHIFT,
+                              method="bounds")
+    A = [int(a) for a in run.run().cpu().numpy()]
+    assert run.used == "bounds"
+    C = _dense(X, shape, beta, ls, kind)
+    rA, _, rdci = op.placement_window_precision(C, k, shape, cutoff)
+    assert A == rA
+    np.testing.assert_allclose(run.greedy.pick_delta[:k].cpu().numpy(),
+                               [rdci[a, i] for i, a in enumerate(rA)], rtol=1e-10)
+    assert k <= run.greedy.refinements <= 4 * k
+
+
+@pytest.mark.parametrize("shape,beta,kind", [
+    ((12, 11, 10), 4.0, "eq"),
+    ((9, 10, 11), 4.0, "matern52"),
+    ((3, 4, 30), 4.0, "matern12"),
+])
+def test_bounds_bracket_dense_inverse(shape, beta, kind):
+    """vgposp_exact_bounds: g_K <= Q_yy <= qhi, with qhi within 4 rho^2K (+ margin) of Q_yy."""
+    from vgposp_amd.sparse_placement import ExactWindowGreedy, TaperProblem
+    X, ls = _grid(shape, seed=sum(shape) + 1)
+    C = _dense(X, shape, beta, ls, kind) + 1e-6 * np.eye(len(X))
+    ref = np.diag(np.linalg.inv(C))
+    prob = TaperProblem(X, shape, beta, kind, ls=ls, diag_shift=SHIFT)
+    g = ExactWindowGreedy(prob, 4, 3)
+    q = torch.zeros(prob.n, dtype=torch.float64, device="cuda")
+    K, scale, width = g.bound_qdiag(q)
+    hi = q.cpu().numpy()
+    assert np.all(hi >= ref)
+    assert np.all(hi <= ref * scale * (1 + 1e-13))
+    assert width <= 1e-6
+    # the same bounds slab by slab
+    q2 = torch.zeros_like(q)
+    n = prob.n
+    for c0, c1 in ((0, n // 3), (n // 3, n - 5), (n - 5, n)):
+        g.bound_qdiag(q2, c0, c1)
+    assert torch.equal(q, q2)
+
+
+def test_bounds_refuse_without_diagonal_dominance():
+    """beta = 2.5: the Gershgorin bounds of the tapered covariance do not bracket its spectrum away
+    from 0, so the bounded form refuses and 'auto' takes the selected inverse."""
+    from vgposp_amd.sparse_placement import ExactTaperPlacement
+    shape = (9, 9, 9)
+    X, ls = _grid(shape, seed=5)
+    run = ExactTaperPlacement(X, shape, 6, 3, 2.5, ls=ls, diag_shift=SHIFT, method="bounds")
+    with pytest.raises(ValueError):
+        run.run()
+    run = ExactTaperPlacement(X, shape, 6, 3, 2.5, ls=ls, diag_shift=SHIFT, leaf=64)
+    A = [int(a) for a in run.run().cpu().numpy()]
+    assert run.used == "selinv"
+    rA, _, _ = op.placement_window_precision(_dense(X, shape, 2.5, ls), 6, shape, 3)
+    assert A == rA
 
 
 def test_exact_alg3_matches_pinv_oracle_tiny():
@@ -109,7 +178,12 @@ def test_exact_alg3_matches_dense_engine(n):
     shape = (n, n, n)
     X, ls = _grid(shape, seed=n)
     k = 50
-    A, deltas, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT)
+    A, deltas, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
+                                                 method="selinv")
+    B, deltas_b, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
+                                                   method="bounds")
+    assert [int(a) for a in A] == [int(a) for a in B]
+    np.testing.assert_allclose(deltas_b, deltas, rtol=1e-12)
     N = len(X)
     S = torch.empty((1, N, N), dtype=torch.float64, device="cuda")
     linalg.kernel_matrix("eq", X, None, 1.0, ls, diag_shift=SHIFT, out=S)
@@ -120,7 +194,7 @@ def test_exact_alg3_matches_dense_engine(n):
     assert [int(a) for a in A] == [int(a) for a in dense]
 
 
-def _two_rank_worker(rank, world, port, shape, k, out):
+def _two_rank_worker(rank, world, port, shape, k, out, method):
     import os
 
     import torch.distributed as dist
@@ -132,16 +206,18 @@ def _two_rank_worker(rank, world, port, shape, k, out):
         from vgposp_amd.sparse_placement import tapered_placement_algorithm_3
         X, ls = _grid(shape, seed=4)
         A, d, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
-                                                leaf=128)
+                                                leaf=128, method=method)
         out[rank] = ([int(a) for a in A], [float(v) for v in d])
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_exact_alg3_ranks_on_one_gpu(world):
-    """The multi-rank C4 path (subtree-to-subcube selected inverse, transfers host-staged over
-    gloo, every rank on cuda:0) gives the single-rank picks and deltas bit for bit."""
+@pytest.mark.parametrize("world,method", [(2, "selinv"), (4, "selinv"), (2, "bounds"),
+                                          (3, "bounds")])
+def test_exact_alg3_ranks_on_one_gpu(world, method):
+    """The multi-rank C4 paths (subtree-to-subcube selected inverse, or the bounds sharded by
+    candidate slabs and all-gathered; transfers host-staged over gloo, every rank on cuda:0) give
+    the single-rank picks and deltas bit for bit."""
     import socket
 
     import torch.multiprocessing as mp
@@ -149,7 +225,7 @@ def test_exact_alg3_ranks_on_one_gpu(world):
     shape, k = (16, 14, 12), 20
     X, ls = _grid(shape, seed=4)
     A1, d1, _ = tapered_placement_algorithm_3(X, k, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
-                                              leaf=128)
+                                              leaf=128, method=method)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -157,14 +233,15 @@ def test_exact_alg3_ranks_on_one_gpu(world):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     out = mgr.dict()
-    mp.start_processes(_two_rank_worker, args=(world, port, shape, k, out), nprocs=world,
+    mp.start_processes(_two_rank_worker, args=(world, port, shape, k, out, method), nprocs=world,
                        join=True, start_method="spawn")
     for r in range(world):
         assert out[r][0] == [int(a) for a in A1]
         np.testing.assert_allclose(out[r][1], d1, rtol=1e-13)
 
 
-def test_exact_128cube_regression():
+@pytest.mark.parametrize("method", ["bounds", "selinv"])
+def test_exact_128cube_regression(method):
     """Config C4 at full size (128^3, k = 50) reproduces the picks committed in
     tests/golden/c4_picks.json (written by tools/bench_exact.py with PICKS_OUT; the same sequence
     the 16^3-40^3 tests tie to the dense algorithm 3).  A regression pin, not a reference
@@ -176,5 +253,6 @@ def test_exact_128cube_regression():
     with open(os.path.join(os.path.dirname(__file__), "golden", "c4_picks.json")) as f:
         want = json.load(f)["picks"]
     X, shape, ls = c4_grid()
-    A, _, _ = tapered_placement_algorithm_3(X, 50, shape, 3, 4.0, ls=ls, diag_shift=SHIFT)
+    A, _, _ = tapered_placement_algorithm_3(X, 50, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
+                                            method=method)
     assert [int(a) for a in A] == want

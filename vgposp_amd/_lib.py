@@ -144,11 +144,17 @@ SIGNATURES = {
                                    _c_void_p, _c_void_p]),
     "vgposp_front_diag": (_i32, [_c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p]),
     "vgposp_exact_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32, _i32, _i32]),
-    "vgposp_exact_prepare": (_i32, _EXACT + [_c_void_p]),
+    "vgposp_exact_prepare": (_i32, _EXACT + [_i32, _c_void_p]),
     "vgposp_exact_round": (_i32, _EXACT + [_i32, _i32, _c_void_p, _c_void_p, _f64, _c_void_p]),
-    "vgposp_exact_buffers": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
-                                    ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p),
-                                    ctypes.POINTER(_c_void_p)]),
+    "vgposp_exact_coef": (_i32, _EXACT + [_c_void_p]),
+    "vgposp_exact_bounds": (_i32, _EXACT + [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _f64,
+                                            _i64, _i64, _c_void_p]),
+    "vgposp_exact_argmax": (_i32, _EXACT + [_c_void_p]),
+    "vgposp_exact_refine": (_i32, _EXACT + [_i32, _c_void_p, _f64, _c_void_p]),
+    "vgposp_exact_pick": (_i32, _EXACT + [_i32, _i32, _c_void_p, _c_void_p, _c_void_p]),
+    "vgposp_exact_update": (_i32, _EXACT + [_i32, _c_void_p, _c_void_p]),
+    "vgposp_exact_buffers": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32]
+                             + [ctypes.POINTER(_c_void_p)] * 6),
     "vgposp_adam_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64, _f64,
                                   _f64, _f64, _c_void_p, _f64, _c_void_p]),
     "vgposp_prof_enable": (_i32, [_i32]),

@@ -20,7 +20,21 @@
 //
 // Every launch only enqueues work: the pick lives in device memory (picks[round]) and every
 // later kernel reads it there, so the whole run is free of host synchronisation.
+//
+// Bounded-lazy form (vgposp_exact_bounds / _argmax / _refine / _pick / _update): diag(Q) is not
+// factored at all.  For every candidate y, K steps of CG on (S + eps I) x = e_y from x = 0 give
+// g_K = sum_i alpha_i |r_i|^2 = e_y^T x_K <= Q_yy, and Q_yy - g_K = |x* - x_K|_A^2
+// <= 4 rho^(2K) Q_yy (rho from a Gershgorin bound on the spectrum), so
+// Q_yy <= g_K / (1 - 4 rho^(2K)).  The K-step Krylov vectors of e_y live on the nodes within K
+// stencil steps of y (a few hundred), so one wave runs one candidate's K steps in registers + LDS.
+// The cache then holds UPPER BOUNDS of the reference's cached deltas (delta is increasing in
+// P_yy); whenever the arg-max lands on a candidate whose Q_yy is only bounded, the host refines
+// it: its full CG column (the same Krylov-box solve a pick gets) gives Q_yy, and its cache entry
+// becomes the reference's value (re-scored with the A of its last window re-score, lastA[y]).
+// The arg-max is only taken when it lands on a refined candidate, so the picks are the
+// reference's, and every pick's column is already there when it is picked.
 #include <cmath>
+#include <type_traits>
 
 #include "common.h"
 #include "psd.h"
@@ -54,9 +68,17 @@ struct ExactWS {
   int* cgstate;       // [4]: done flag, iterations of the last solve
   double* LS;         // [kmax][kmax] chol(S_AA + eps I)
   double* LQ;         // [kmax][kmax] chol(Q_AA)
-  double* Qcols;      // [kmax][bv]: Q e_{a_t} on pick t's box (zero outside it)
+  double* Qcols;      // [nslots][bv]: Q e_c on candidate c's box (zero outside it)
+  int* slot_of_round; // [kmax]: the column slot of pick t
+  unsigned char* qexact;  // [n]: 1 = qdiag[y] is Q_yy, 0 = an upper bound of it
+  unsigned char* lastA;   // [n]: |A| when y's cache entry was last scored (0: round 0)
+  long long* cand;    // [2]: the arg-max candidate of vgposp_exact_argmax
+  double* gersh;      // [2 + 2 CG_BLOCKS]: lambda_min / lambda_max bounds, then partials
   size_t bytes;
 };
+
+// column slots: one per pick, as many again for refined candidates that are not (yet) picked
+__host__ __device__ __forceinline__ int exact_slots(int kmax) { return 2 * kmax; }
 
 constexpr int CG_MAXIT = 512;
 
@@ -88,14 +110,19 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
   w.p0 = (double*)take(8 * (size_t)bv);
   w.p1 = (double*)take(8 * (size_t)bv);
   w.q = (double*)take(8 * (size_t)bv);
-  w.boxlo = (long long*)take(8 * 3 * (size_t)kmax);
+  w.boxlo = (long long*)take(8 * 3 * (size_t)exact_slots(kmax));
   w.part_pq = (double*)take(8 * CG_BLOCKS);
   w.part_rr = (double*)take(8 * CG_BLOCKS);
   w.rr = (double*)take(8 * (CG_MAXIT + 2));
   w.cgstate = (int*)take(16);
   w.LS = (double*)take(8 * (size_t)kmax * kmax);
   w.LQ = (double*)take(8 * (size_t)kmax * kmax);
-  w.Qcols = (double*)take(8 * (size_t)kmax * bv);
+  w.Qcols = (double*)take(8 * (size_t)exact_slots(kmax) * bv);
+  w.slot_of_round = (int*)take(4 * (size_t)kmax);
+  w.qexact = (unsigned char*)take((size_t)n);
+  w.lastA = (unsigned char*)take((size_t)n);
+  w.cand = (long long*)take(16);
+  w.gersh = (double*)take(8 * (2 + 2 * (size_t)CG_BLOCKS));
   w.bytes = off;
   return w;
 }
@@ -133,17 +160,34 @@ __device__ __forceinline__ double sigma_off(const EArgs& a, long long i, long lo
   return t * kfun<KIND>(d0 * d0 + d1 * d1 + d2 * d2, a.tla, a.inv_ls, a.inv_ls2);
 }
 
-// Q e_{a_r} at grid node y: its box value, 0 outside the box.
-__device__ __forceinline__ double qcol_at(const ExactWS& w, int r, long long y, long long I1,
-                                          long long I2) {
-  const long long* lo = w.boxlo + 3 * r;
+// Column slot `slot` at grid node y: its box value, 0 outside the box.
+__device__ __forceinline__ double qslot_at(const ExactWS& w, int slot, long long y, long long I1,
+                                           long long I2) {
+  const long long* lo = w.boxlo + 3 * slot;
   const long long l0 = y / (I1 * I2) - lo[0], l1 = (y / I2) % I1 - lo[1], l2 = y % I2 - lo[2];
   if (l0 < 0 || l0 >= w.b0 || l1 < 0 || l1 >= w.b1 || l2 < 0 || l2 >= w.b2) return 0.0;
-  return w.Qcols[(size_t)r * (w.b0 * w.b1 * w.b2) + (l0 * w.b1 + l1) * w.b2 + l2];
+  return w.Qcols[(size_t)slot * (w.b0 * w.b1 * w.b2) + (l0 * w.b1 + l1) * w.b2 + l2];
+}
+
+// Q e_{a_r} (pick r's column) at grid node y.
+__device__ __forceinline__ double qcol_at(const ExactWS& w, int r, long long y, long long I1,
+                                          long long I2) {
+  return qslot_at(w, w.slot_of_round[r], y, I1, I2);
 }
 
 __device__ __forceinline__ double delta_of(double nom, double den, double thr) {
   return (fabs(nom) < thr || fabs(den) < thr) ? 0.0 : nom / den;
+}
+
+// The cached delta from nom and P_yy = Q_yy - |LQ^-1 q_Ay|^2; with `exact` false P is an upper
+// bound of P_yy and the result an upper bound of the delta (denom = 1/P - eps decreases in P; a
+// denominator that may still reach the threshold is bounded by it).
+__device__ __forceinline__ double delta_from(double nom, double P, bool exact, double eps,
+                                             double thr) {
+  const double den = 1.0 / P - eps;
+  if (exact) return delta_of(nom, den, thr);
+  if (fabs(nom) < thr) return 0.0;
+  return nom / fmax(den, thr);
 }
 
 // coef[i][0] = S_ii + eps, coef[i][1 + o] = S(i, i + off_o) (0 outside the grid)
@@ -165,15 +209,256 @@ __global__ __launch_bounds__(256) void exact_coef_kernel(EArgs a, double* __rest
   }
 }
 
-// Round 0 (snippets_a3.py:77-124): A empty, nom = s_yy, denom = 1 / Q_yy - eps.
+// Gershgorin bounds of the spectrum of S + eps I from the coefficient table: per row
+// c_ii -/+ sum_j |c_ij|; block partials of (min lower, max upper), then one block reduces them.
+__global__ __launch_bounds__(256) void exact_gersh_kernel(const double* __restrict__ coef,
+                                                          long long n, int m, double* part) {
+  __shared__ double rl[4], rh[4];
+  double lo = INFINITY, hi = -INFINITY;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const double* c = coef + i * m;
+    double s = 0.0;
+    for (int o = 1; o < m; ++o) s += fabs(c[o]);
+    lo = fmin(lo, c[0] - s);
+    hi = fmax(hi, c[0] + s);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    rl[threadIdx.x >> 6] = lo;
+    rh[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 + blockIdx.x] = fmin(fmin(rl[0], rl[1]), fmin(rl[2], rl[3]));
+    part[2 + CG_BLOCKS + blockIdx.x] = fmax(fmax(rh[0], rh[1]), fmax(rh[2], rh[3]));
+  }
+}
+
+__global__ __launch_bounds__(64) void exact_gersh_final_kernel(double* part, int np) {
+  double lo = INFINITY, hi = -INFINITY;
+  for (int i = threadIdx.x; i < np; i += 64) {
+    lo = fmin(lo, part[2 + i]);
+    hi = fmax(hi, part[2 + CG_BLOCKS + i]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+  }
+  if (threadIdx.x == 0) {
+    part[0] = lo;
+    part[1] = hi;
+  }
+}
+
+// Upper bounds of Q_yy for y in [c0, c1): K CG steps on (S + eps I) x = e_y from x = 0, one wave
+// per candidate.  The nodes within K stencil steps of y are a host table sorted by step distance
+// (tab_off [T][3] offsets, tab_cnt[d] = nodes within d steps, tab_nb [T][m1] = table position of
+// node + off_o or -1); lane l holds nodes l, l + 64, ... in registers, p is exchanged through a
+// wave-private LDS vector.  Step it touches only the tab_cnt[it + 1] nodes A p_it can reach.
+// qhi[y] = hi_scale * sum_i alpha_i |r_i|^2, hi_scale = (1 + margin) / (1 - 4 rho^(2K)).
+constexpr int BND_T = 256;
+constexpr int BND_WAVES = BND_T / 64;
+constexpr int BND_SMAX = 14;
+constexpr int BND_TMAX = 64 * BND_SMAX;
+constexpr int BND_NBMAX = 8192;
+
+__global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
+    const double* __restrict__ coef, long long I0, long long I1, long long I2, int m1,
+    const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
+    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, long long c0, long long c1,
+    double* __restrict__ qhi) {
+  __shared__ double plds[BND_WAVES][BND_TMAX];
+  __shared__ short nbl[BND_NBMAX];
+  __shared__ short offl[3 * BND_TMAX];
+  __shared__ int cntl[BND_SMAX * 4 + 1];
+  for (int i = threadIdx.x; i < T * m1; i += BND_T) nbl[i] = (short)tab_nb[i];
+  for (int i = threadIdx.x; i < 3 * T; i += BND_T) offl[i] = (short)tab_off[i];
+  for (int i = threadIdx.x; i <= K; i += BND_T) cntl[i] = tab_cnt[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* pl = plds[wave];
+  const int m = m1 + 1;
+  for (long long y = c0 + (long long)blockIdx.x * BND_WAVES + wave; y < c1;
+       y += (long long)gridDim.x * BND_WAVES) {
+    const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
+    int gi[BND_SMAX];  // grid index (n < 2^31, checked by the caller) or -1
+    double r[BND_SMAX], p[BND_SMAX], q[BND_SMAX];
+#pragma unroll
+    for (int s = 0; s < BND_SMAX; ++s) {
+      const int j = s * 64 + lane;
+      gi[s] = -1;
+      r[s] = (j == 0) ? 1.0 : 0.0;   // node 0 is y itself
+      p[s] = r[s];
+      if (j < T) {
+        const long long g0 = y0 + offl[3 * j], g1 = y1 + offl[3 * j + 1], g2 = y2 + offl[3 * j + 2];
+        if (g0 >= 0 && g0 < I0 && g1 >= 0 && g1 < I1 && g2 >= 0 && g2 < I2)
+          gi[s] = (int)((g0 * I1 + g1) * I2 + g2);
+        pl[j] = r[s];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double rr = 1.0, g = 0.0;
+    for (int it = 0; it < K; ++it) {
+      const int cnt = cntl[it + 1];
+      double pq = 0.0;
+#pragma unroll
+      for (int s = 0; s < BND_SMAX; ++s) {
+        const int j = s * 64 + lane;
+        q[s] = 0.0;
+        if (s * 64 < cnt && j < cnt && gi[s] >= 0) {
+          const double* c = coef + (size_t)gi[s] * m;
+          double acc = c[0] * p[s];
+          const short* nb = nbl + j * m1;
+          for (int o = 0; o < m1; ++o) {
+            const int jn = nb[o];
+            if (jn >= 0) acc = fma(c[1 + o], pl[jn], acc);
+          }
+          q[s] = acc;
+          pq = fma(p[s], acc, pq);
+        }
+      }
+      pq = wave_sum(pq);
+      const double alpha = rr / pq;
+      g = fma(alpha, rr, g);
+      if (it + 1 == K) break;
+      double rn = 0.0;
+#pragma unroll
+      for (int s = 0; s < BND_SMAX; ++s) {
+        r[s] = fma(-alpha, q[s], r[s]);
+        rn = fma(r[s], r[s], rn);
+      }
+      rn = wave_sum(rn);
+      const double beta = rn / rr;
+      rr = rn;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int s = 0; s < BND_SMAX; ++s) {
+        const int j = s * 64 + lane;
+        p[s] = fma(beta, p[s], r[s]);
+        if (j < cnt) pl[j] = p[s];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) qhi[y] = g * hi_scale;
+  }
+}
+
+// The same bounds with the stencil size M1 and the slots per lane SM compile-time: a candidate's
+// coefficients (SM x (M1 + 1) doubles per lane) are loaded into registers once, all loads in
+// flight together, so its K steps run on registers and LDS only (the generic kernel above waits on
+// one coefficient load at a time).  Neighbours outside the table read a zero LDS entry.
+template <int SM, int M1>
+__global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
+    const double* __restrict__ coef, long long I0, long long I1, long long I2,
+    const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
+    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, long long c0, long long c1,
+    double* __restrict__ qhi) {
+  constexpr int TP = SM * 64;
+  __shared__ double plds[BND_WAVES][TP + 1];
+  __shared__ short nbl[TP * M1];
+  __shared__ short offl[3 * TP];
+  __shared__ int cntl[4 * BND_SMAX + 1];
+  for (int i = threadIdx.x; i < TP * M1; i += BND_T) {
+    const int v = i < T * M1 ? tab_nb[i] : -1;
+    nbl[i] = (short)(v >= 0 ? v : TP);
+  }
+  for (int i = threadIdx.x; i < 3 * TP; i += BND_T) offl[i] = (short)(i < 3 * T ? tab_off[i] : 0);
+  for (int i = threadIdx.x; i <= K; i += BND_T) cntl[i] = tab_cnt[i];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* pl = plds[wave];
+  if (lane == 0) pl[TP] = 0.0;
+  __syncthreads();
+  constexpr int M = M1 + 1;
+  for (long long y = c0 + (long long)blockIdx.x * BND_WAVES + wave; y < c1;
+       y += (long long)gridDim.x * BND_WAVES) {
+    const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
+    double c[SM][M];
+    double r[SM], p[SM], q[SM];
+#pragma unroll
+    for (int s = 0; s < SM; ++s) {
+      const int j = s * 64 + lane;
+      long long gi = -1;
+      if (j < T) {
+        const long long g0 = y0 + offl[3 * j], g1 = y1 + offl[3 * j + 1], g2 = y2 + offl[3 * j + 2];
+        if (g0 >= 0 && g0 < I0 && g1 >= 0 && g1 < I1 && g2 >= 0 && g2 < I2)
+          gi = (g0 * I1 + g1) * I2 + g2;
+      }
+#pragma unroll
+      for (int o = 0; o < M; ++o) c[s][o] = gi >= 0 ? coef[gi * M + o] : 0.0;
+      r[s] = (j == 0) ? 1.0 : 0.0;
+      p[s] = r[s];
+      pl[j] = r[s];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double rr = 1.0, g = 0.0;
+    for (int it = 0; it < K; ++it) {
+      const int cnt = cntl[it + 1];
+      double pq = 0.0;
+#pragma unroll
+      for (int s = 0; s < SM; ++s) {
+        q[s] = 0.0;
+        if (s * 64 < cnt) {
+          const int j = s * 64 + lane;
+          double acc = c[s][0] * p[s];
+#pragma unroll
+          for (int o = 0; o < M1; ++o) acc = fma(c[s][1 + o], pl[nbl[j * M1 + o]], acc);
+          q[s] = j < cnt ? acc : 0.0;
+          pq = fma(p[s], q[s], pq);
+        }
+      }
+      pq = wave_sum(pq);
+      const double alpha = rr / pq;
+      g = fma(alpha, rr, g);
+      if (it + 1 == K) break;
+      double rn = 0.0;
+#pragma unroll
+      for (int s = 0; s < SM; ++s) {
+        r[s] = fma(-alpha, q[s], r[s]);
+        rn = fma(r[s], r[s], rn);
+      }
+      rn = wave_sum(rn);
+      const double beta = rn / rr;
+      rr = rn;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int s = 0; s < SM; ++s) {
+        p[s] = fma(beta, p[s], r[s]);
+        if (s * 64 < cnt) pl[s * 64 + lane] = p[s];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) qhi[y] = g * hi_scale;
+  }
+}
+
+// Round 0 (snippets_a3.py:77-124): A empty, nom = s_yy, denom = 1 / Q_yy - eps (an upper bound of
+// the delta where qexact[y] = 0).
 template <int KIND>
 __global__ __launch_bounds__(256) void exact_score_kernel(EArgs a, const double* __restrict__ qdiag,
+                                                          const unsigned char* __restrict__ qexact,
                                                           double* __restrict__ cache) {
   const long long y = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (y >= a.n) return;
   const double nom = sigma_diag<KIND>(a);
-  const double den = 1.0 / qdiag[y] - a.jitter;
-  cache[y] = delta_of(nom, den, a.thr);
+  cache[y] = delta_from(nom, qdiag[y], qexact[y] != 0, a.jitter, a.thr);
 }
 
 // One wave: key of block b (entries [b EB, (b+1) EB) of the cache, selected ones excluded).
@@ -234,13 +519,9 @@ __global__ __launch_bounds__(256) void exact_super_keys_kernel(const double* bva
   if (sb < nsb) wave_super_key(bval, bidx, nblk, sb, sval, sidx);
 }
 
-// Workgroup-wide arg-max over the superblock keys -> the pick of round `round`
-// (placement_algorithm2.py:24-50 via sparse_argmax_cache_linear); A <- A u {y*}, the cache entry of
-// y* <- 0 (snippets_a3.py:162-168), its block keys refreshed; CG set up for q = Q e_{y*}.
-__global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
-    double* cache, unsigned char* sel, long long I0, long long I1, long long I2, ExactWS w,
-    long long nblk, long long nsb, int round, long long* picks, double* pick_delta, int solve) {
-  const long long n = I0 * I1 * I2;
+// Workgroup-wide arg-max over the superblock keys (placement_algorithm2.py:24-50 via
+// sparse_argmax_cache_linear); every thread returns it.
+__device__ long long block_argmax(const ExactWS& w, long long nsb) {
   __shared__ double sv[SEL_THREADS / 64];
   __shared__ long long si[SEL_THREADS / 64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -262,37 +543,105 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
     v = lane < SEL_THREADS / 64 ? sv[lane] : 0.0;
     idx = lane < SEL_THREADS / 64 ? si[lane] : -1;
     wave_keymax(v, idx);
-    if (lane == 0) {
-      si[0] = idx;
-      picks[round] = idx;
-      if (pick_delta) pick_delta[round] = idx >= 0 ? cache[idx] : 0.0;
-      if (idx >= 0) {
-        sel[idx] = 1;
-        cache[idx] = 0.0;
-        if (solve) {
-          // the column's box: [a - H, a + H] per axis, shifted inside the grid
-          const long long a0 = idx / (I1 * I2), a1 = (idx / I2) % I1, a2 = idx % I2;
-          const long long lo0 = min(max(a0 - w.H, 0LL), I0 - w.b0);
-          const long long lo1 = min(max(a1 - w.H, 0LL), I1 - w.b1);
-          const long long lo2 = min(max(a2 - w.H, 0LL), I2 - w.b2);
-          w.boxlo[3 * round] = lo0;
-          w.boxlo[3 * round + 1] = lo1;
-          w.boxlo[3 * round + 2] = lo2;
-          w.r[((a0 - lo0) * w.b1 + (a1 - lo1)) * w.b2 + (a2 - lo2)] = 1.0;
-        }
-      }
-      w.rr[0] = 1.0;
-      w.cgstate[0] = 0;
-      w.cgstate[1] = 0;
+    if (lane == 0) si[0] = idx;
+  }
+  __syncthreads();
+  const long long r = si[0];
+  __syncthreads();
+  return r;
+}
+
+// Refresh the block key and superblock key of candidate y (one wave).
+__device__ __forceinline__ void wave_refresh_keys(const double* cache, const unsigned char* sel,
+                                                  const ExactWS& w, long long n, long long nblk,
+                                                  long long y) {
+  const long long b = y / EB;
+  wave_block_key(cache, sel, n, b, w.bval, w.bidx);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  wave_super_key(w.bval, w.bidx, nblk, b / ESB, w.sval, w.sidx);
+}
+
+// The pick of round `round` (selected-inverse path): A <- A u {y*}, the cache entry of y* <- 0
+// (snippets_a3.py:162-168), its keys refreshed; CG set up for q = Q e_{y*} in slot `round`.
+__global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
+    double* cache, unsigned char* sel, long long I0, long long I1, long long I2, ExactWS w,
+    long long nblk, long long nsb, int round, long long* picks, double* pick_delta, int solve) {
+  const long long n = I0 * I1 * I2;
+  const long long a = block_argmax(w, nsb);
+  if (threadIdx.x == 0) {
+    picks[round] = a;
+    if (pick_delta) pick_delta[round] = a >= 0 ? cache[a] : 0.0;
+    w.slot_of_round[round] = round;
+    if (a >= 0) {
+      sel[a] = 1;
+      cache[a] = 0.0;
     }
   }
   __syncthreads();
-  const long long a = si[0];
-  if (a < 0) return;
-  const long long b = a / EB;
-  if (wave == 0) wave_block_key(cache, sel, n, b, w.bval, w.bidx);
+  if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
+}
+
+// Bounded-lazy path: the arg-max candidate -> cand[0] (nothing else changes).
+__global__ __launch_bounds__(SEL_THREADS) void exact_argmax_kernel(ExactWS w, long long nsb) {
+  const long long a = block_argmax(w, nsb);
+  if (threadIdx.x == 0) w.cand[0] = a;
+}
+
+// Bounded-lazy path: pick cand[0] (refined, its column in `slot`) as pick `round`.
+__global__ __launch_bounds__(64) void exact_pick_kernel(double* cache, unsigned char* sel,
+                                                        long long n, ExactWS w, long long nblk,
+                                                        int round, int slot, long long* picks,
+                                                        double* pick_delta) {
+  const long long a = w.cand[0];
+  if (threadIdx.x == 0) {
+    picks[round] = a;
+    if (pick_delta) pick_delta[round] = a >= 0 ? cache[a] : 0.0;
+    w.slot_of_round[round] = slot;
+    if (a >= 0) {
+      sel[a] = 1;
+      cache[a] = 0.0;
+    }
+  }
   __syncthreads();
-  if (wave == 0) wave_super_key(w.bval, w.bidx, nblk, b / ESB, w.sval, w.sidx);
+  if (a >= 0) wave_refresh_keys(cache, sel, w, n, nblk, a);
+}
+
+// Start the CG solve of S x = e_c (c = *center) into column slot `slot`: r, p0, p1 and the
+// column zeroed except r = e_c, the box [c - H, c + H] per axis shifted inside the grid ->
+// boxlo[slot], rr[0] = 1, CG state cleared (marked done when there is no candidate).
+__global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long long I0, long long I1,
+                                                             long long I2, int slot,
+                                                             const long long* center,
+                                                             double* __restrict__ x) {
+  const long long c = *center;
+  const long long bv = w.b0 * w.b1 * w.b2;
+  long long lc = -1;
+  if (c >= 0) {
+    const long long a0 = c / (I1 * I2), a1 = (c / I2) % I1, a2 = c % I2;
+    const long long lo0 = min(max(a0 - w.H, 0LL), I0 - w.b0);
+    const long long lo1 = min(max(a1 - w.H, 0LL), I1 - w.b1);
+    const long long lo2 = min(max(a2 - w.H, 0LL), I2 - w.b2);
+    lc = ((a0 - lo0) * w.b1 + (a1 - lo1)) * w.b2 + (a2 - lo2);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      w.boxlo[3 * slot] = lo0;
+      w.boxlo[3 * slot + 1] = lo1;
+      w.boxlo[3 * slot + 2] = lo2;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    w.rr[0] = 1.0;
+    w.cgstate[0] = c >= 0 ? 0 : 1;
+    w.cgstate[1] = 0;
+  }
+  for (long long l = (long long)blockIdx.x * 256 + threadIdx.x; l < bv;
+       l += (long long)gridDim.x * 256) {
+    w.r[l] = l == lc ? 1.0 : 0.0;
+    w.p0[l] = 0.0;
+    w.p1[l] = 0.0;
+    x[l] = 0.0;
+  }
 }
 
 // Deterministic block reduction of the first `np` partials (every block computes the same sum).
@@ -324,8 +673,8 @@ __device__ __forceinline__ void block_partial(double v, double* part, double* re
 }
 
 // Box-local node l -> (grid coordinates, inside the active region of iteration it).  The
-// iterate's support after `it` steps lies within `it` stencil radii of the pick in every axis; the
-// kernels skip the rest of the box (its entries are and stay exactly zero).
+// iterate's support after `it` steps lies within `it` stencil radii of the centre in every axis;
+// the kernels skip the rest of the box (its entries are and stay exactly zero).
 struct BoxNode {
   long long g0, g1, g2;
   bool active;
@@ -346,14 +695,17 @@ __device__ __forceinline__ BoxNode box_node(const ExactWS& w, long long l, const
 // CG iteration it, part A: beta from the last residual norms, p_it = r + beta p_{it-1} (computed
 // for the neighbours on the fly, written for this thread's own nodes), q = (S + eps I) p_it and
 // the partials of p_it . q.  Converged (|r|^2 <= tol2) -> every block returns; block 0 records it.
+// The solve is for the column of *center into slot `slot`.
 __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I0, long long I1,
                                                           long long I2, const int* offs, int m1,
-                                                          int srad, int round,
-                                                          const long long* picks, int it,
-                                                          double tol2) {
+                                                          int srad, int slot,
+                                                          const long long* center, int it,
+                                                          int np_prev, double tol2) {
   __shared__ double red[CG_T / 64];
   if (w.cgstate[0]) return;
-  const double rr = w.rr[it];
+  // |r_it|^2 from the B kernel's partials (every block sums them in the same order)
+  const double rr = it == 0 ? w.rr[0] : sum_partials(w.part_rr, np_prev, red);
+  if (it > 0 && blockIdx.x == 0 && threadIdx.x == 0) w.rr[it] = rr;
   if (rr <= tol2) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       w.cgstate[0] = 1;
@@ -364,9 +716,9 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   const double beta = it == 0 ? 0.0 : rr / w.rr[it - 1];
   const double* pold = (it & 1) ? w.p0 : w.p1;  // p_{it-1}
   double* pnew = (it & 1) ? w.p1 : w.p0;        // p_it
-  const long long a = picks[round];
+  const long long a = *center;
   const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
-  const long long* lo = w.boxlo + 3 * round;
+  const long long* lo = w.boxlo + 3 * slot;
   const long long bv = w.b0 * w.b1 * w.b2;
   const long long rad = min((long long)(it + 1) * srad, w.H);
   const int m = m1 + 1;
@@ -396,17 +748,17 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
 
 // CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2.
 __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I1, long long I2,
-                                                          int srad, int round,
-                                                          const long long* picks, int it,
+                                                          int srad, int slot,
+                                                          const long long* center, int it,
                                                           double* __restrict__ x) {
   __shared__ double red[CG_T / 64];
   if (w.cgstate[0]) return;
   const double pq = sum_partials(w.part_pq, (int)gridDim.x, red);  // the A kernel's grid
   const double alpha = w.rr[it] / pq;
   const double* p = (it & 1) ? w.p1 : w.p0;
-  const long long a = picks[round];
+  const long long a = *center;
   const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
-  const long long* lo = w.boxlo + 3 * round;
+  const long long* lo = w.boxlo + 3 * slot;
   const long long bv = w.b0 * w.b1 * w.b2;
   const long long rad = min((long long)(it + 1) * srad, w.H);
   double acc = 0.0;
@@ -420,108 +772,170 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
   block_partial(acc, w.part_rr, red);
 }
 
-// |r|^2 of iteration it + 1 (one block; every CG_A block then reads it).
-__global__ __launch_bounds__(CG_T) void exact_cg_c_kernel(ExactWS w, int it, int np) {
-  __shared__ double red[CG_T / 64];
-  if (w.cgstate[0]) return;
-  const double rr = sum_partials(w.part_rr, np, red);
-  if (threadIdx.x == 0) w.rr[it + 1] = rr;
-}
-
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
 
-// After q_t = Q e_{a_t}: append row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I), then
-// re-score the window of a_t (snippets_a3.py:190-303; candidates in A -> 0) and refresh the block
-// and superblock keys it touched.  One workgroup.
+// The cached delta of candidate y given the first nA picks (rows 0 .. nA-1 of LQ / LS, in global
+// memory), one wave: nominator s_yy - |LS^-1 s_Ay|^2, P = qyy - |LQ^-1 q_Ay|^2.  Lane s holds the
+// forward-substitution unknowns z_s and z_{s+64}; every lane returns the delta.
 template <int KIND>
-__global__ __launch_bounds__(SEL_THREADS) void exact_update_kernel(
-    EArgs a, const double* __restrict__ qdiag, double* cache, const unsigned char* sel, ExactWS w,
-    long long nblk, int round, const long long* picks) {
+__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const long long* picks, int nA,
+                               long long y, double qyy, bool exact) {
+  const int lane = threadIdx.x & 63;
+  const int km = a.kmax;
+  double vs0 = 0.0, vq0 = 0.0, vs1 = 0.0, vq1 = 0.0;
+  if (lane < nA) {
+    vs0 = sigma_off<KIND>(a, picks[lane], y);
+    vq0 = qcol_at(w, lane, y, a.I1, a.I2);
+  }
+  if (lane + 64 < nA) {
+    vs1 = sigma_off<KIND>(a, picks[lane + 64], y);
+    vq1 = qcol_at(w, lane + 64, y, a.I1, a.I2);
+  }
+  double zs0 = 0.0, zq0 = 0.0, zs1 = 0.0, zq1 = 0.0;
+  for (int r = 0; r < nA; ++r) {
+    const double* ls = w.LS + (size_t)r * km;
+    const double* lq = w.LQ + (size_t)r * km;
+    double ds = 0.0, dq = 0.0;
+    if (lane < r) {
+      ds = ls[lane] * zs0;
+      dq = lq[lane] * zq0;
+    }
+    if (lane + 64 < r) {
+      ds = fma(ls[lane + 64], zs1, ds);
+      dq = fma(lq[lane + 64], zq1, dq);
+    }
+    ds = wave_sum(ds);
+    dq = wave_sum(dq);
+    if (r < 64) {
+      if (lane == r) {
+        zs0 = (vs0 - ds) / ls[r];
+        zq0 = (vq0 - dq) / lq[r];
+      }
+    } else if (lane == r - 64) {
+      zs1 = (vs1 - ds) / ls[r];
+      zq1 = (vq1 - dq) / lq[r];
+    }
+  }
+  const double ns = wave_sum(fma(zs0, zs0, zs1 * zs1));
+  const double nq = wave_sum(fma(zq0, zq0, zq1 * zq1));
+  return delta_from(sigma_diag<KIND>(a) - ns, qyy - nq, exact, a.jitter, a.thr);
+}
+
+// Bounded-lazy path, after the CG column of cand[0] in slot `slot`: Q_cc is now known; the
+// candidate's cache entry becomes the reference's value (scored with the A of its last re-score)
+// and its keys are refreshed.  One wave.
+template <int KIND>
+__global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* qdiag,
+                                                              double* cache, unsigned char* sel,
+                                                              ExactWS w, long long nblk, int slot,
+                                                              const long long* picks) {
+  const long long c = w.cand[0];
+  if (c < 0) return;
+  const double qcc = qslot_at(w, slot, c, a.I1, a.I2);
+  const double d = wave_rescore<KIND>(a, w, picks, (int)w.lastA[c], c, qcc, true);
+  if (threadIdx.x == 0) {
+    qdiag[c] = qcc;
+    w.qexact[c] = 1;
+    cache[c] = d;
+  }
+  __syncthreads();
+  wave_refresh_keys(cache, sel, w, a.n, nblk, c);
+}
+
+// After q_t = Q e_{a_t}, part 1: row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I) (one wave
+// each).
+template <int KIND>
+__global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int round,
+                                                         const long long* picks) {
   __shared__ double rowbuf[2][EX_KMAX];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int km = a.kmax;
   const long long at = picks[round];
   if (at < 0) return;
-  // row `round` of the two factors, one wave each, built in LDS
-  if (wave < 2) {
-    const double* L = wave == 0 ? w.LQ : w.LS;
-    double* row = rowbuf[wave];
-    for (int r = 0; r <= round; ++r) {
-      const long long ar = picks[r];
-      double v;
-      if (wave == 0) v = qcol_at(w, round, ar, a.I1, a.I2);
-      else v = (r == round) ? sigma_diag<KIND>(a) + a.jitter : sigma_off<KIND>(a, at, ar);
-      double acc = 0.0;
-      // off-diagonal: row . L[r][:r];  diagonal (r == round): |row[:r]|^2
-      for (int s = lane; s < r; s += 64)
-        acc = fma(row[s], r == round ? row[s] : L[(size_t)r * km + s], acc);
-      acc = wave_sum(acc);
-      v -= acc;
-      if (lane == 0) row[r] = (r == round) ? sqrt(v) : v / L[(size_t)r * km + r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+  const double* L = wave == 0 ? w.LQ : w.LS;
+  double* row = rowbuf[wave];
+  for (int r = 0; r <= round; ++r) {
+    const long long ar = picks[r];
+    double v;
+    if (wave == 0) v = qcol_at(w, round, ar, a.I1, a.I2);
+    else v = (r == round) ? sigma_diag<KIND>(a) + a.jitter : sigma_off<KIND>(a, at, ar);
+    double acc = 0.0;
+    // off-diagonal: row . L[r][:r];  diagonal (r == round): |row[:r]|^2
+    for (int s = lane; s < r; s += 64)
+      acc = fma(row[s], r == round ? row[s] : L[(size_t)r * km + s], acc);
+    acc = wave_sum(acc);
+    v -= acc;
+    if (lane == 0) row[r] = (r == round) ? sqrt(v) : v / L[(size_t)r * km + r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  __syncthreads();
-  if (t <= round) {
-    w.LQ[(size_t)round * km + t] = rowbuf[0][t];
-    w.LS[(size_t)round * km + t] = rowbuf[1][t];
-  }
-  __syncthreads();
-  // window re-score: one thread per candidate; the new rows are read from LDS
+  double* Lw = wave == 0 ? w.LQ : w.LS;
+  for (int s = lane; s <= round; s += 64) Lw[(size_t)round * km + s] = row[s];
+}
+
+struct Window {
+  long long lo0, lo1, lo2, w0, w1, w2;
+};
+
+__device__ __forceinline__ Window window_of(const EArgs& a, long long at) {
+  Window v;
   const long long ci0 = at / (a.I1 * a.I2), ci1 = (at / a.I2) % a.I1, ci2 = at % a.I2;
-  const long long lo0 = max(ci0 - a.cutoff, 0LL), lo1 = max(ci1 - a.cutoff, 0LL),
-                  lo2 = max(ci2 - a.cutoff, 0LL);
-  const long long w0 = max(min(ci0 + a.cutoff, a.I0) - lo0, 0LL),
-                  w1 = max(min(ci1 + a.cutoff, a.I1) - lo1, 0LL),
-                  w2 = max(min(ci2 + a.cutoff, a.I2) - lo2, 0LL);
-  const long long nw = w0 * w1 * w2;
-  const double syy = sigma_diag<KIND>(a);
-  for (long long e = t; e < nw; e += SEL_THREADS) {
-    const long long y = ((lo0 + e / (w1 * w2)) * a.I1 + lo1 + (e / w2) % w1) * a.I2 + lo2 + e % w2;
-    if (sel[y]) {
-      cache[y] = 0.0;
-      continue;
-    }
-    // nominator |LS^-1 s_Ay|^2, denominator |LQ^-1 q_Ay|^2 (forward substitutions)
-    double zs[EX_KMAX], zq[EX_KMAX];
-    double ns = 0.0, nq = 0.0;
-    for (int r = 0; r <= round; ++r) {
-      const long long ar = picks[r];
-      double vs = sigma_off<KIND>(a, ar, y);
-      double vq = qcol_at(w, r, y, a.I1, a.I2);
-      const double* ls = r == round ? rowbuf[1] : w.LS + (size_t)r * km;
-      const double* lq = r == round ? rowbuf[0] : w.LQ + (size_t)r * km;
-      for (int s = 0; s < r; ++s) {
-        vs = fma(-ls[s], zs[s], vs);
-        vq = fma(-lq[s], zq[s], vq);
-      }
-      vs /= ls[r];
-      vq /= lq[r];
-      zs[r] = vs;
-      zq[r] = vq;
-      ns = fma(vs, vs, ns);
-      nq = fma(vq, vq, nq);
-    }
-    const double nom = syy - ns;
-    const double den = 1.0 / (qdiag[y] - nq) - a.jitter;
-    cache[y] = delta_of(nom, den, a.thr);
+  v.lo0 = max(ci0 - a.cutoff, 0LL);
+  v.lo1 = max(ci1 - a.cutoff, 0LL);
+  v.lo2 = max(ci2 - a.cutoff, 0LL);
+  v.w0 = max(min(ci0 + a.cutoff, a.I0) - v.lo0, 0LL);
+  v.w1 = max(min(ci1 + a.cutoff, a.I1) - v.lo1, 0LL);
+  v.w2 = max(min(ci2 + a.cutoff, a.I2) - v.lo2, 0LL);
+  return v;
+}
+
+// Part 2: re-score the window of a_t (snippets_a3.py:190-303; candidates in A -> 0), one wave per
+// candidate; upper bounds where Q_yy is still only bounded.
+template <int KIND>
+__global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
+                                                           double* cache, const unsigned char* sel,
+                                                           ExactWS w, int round,
+                                                           const long long* picks) {
+  const long long at = picks[round];
+  if (at < 0) return;
+  const Window v = window_of(a, at);
+  const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= v.w0 * v.w1 * v.w2) return;
+  const long long y = ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) * a.I2 +
+                      v.lo2 + e % v.w2;
+  if (sel[y]) {
+    if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
+    return;
   }
-  __syncthreads();
-  if (t == 0) cache[at] = 0.0;
-  __syncthreads();
-  // refresh the block keys of the window rows (each (j0, j1) row is one contiguous i2 run)
-  const long long nrow = w0 * w1;
+  const double d = wave_rescore<KIND>(a, w, picks, round + 1, y, qdiag[y], w.qexact[y] != 0);
+  if ((threadIdx.x & 63) == 0) {
+    cache[y] = d;
+    w.lastA[y] = (unsigned char)(round + 1);
+  }
+}
+
+// Part 3: refresh the block keys of the window rows (each (j0, j1) row is one contiguous i2 run),
+// then their superblock keys.  One workgroup.
+__global__ __launch_bounds__(SEL_THREADS) void exact_window_keys_kernel(EArgs a, const double* cache,
+                                                                        const unsigned char* sel,
+                                                                        ExactWS w, long long nblk,
+                                                                        int round,
+                                                                        const long long* picks) {
+  const long long at = picks[round];
+  if (at < 0) return;
+  const Window v = window_of(a, at);
+  const int wave = threadIdx.x >> 6;
+  const long long nrow = v.w0 * v.w1;
   for (long long rr = wave; rr < nrow; rr += SEL_THREADS / 64) {
-    const long long y0 = ((lo0 + rr / w1) * a.I1 + lo1 + rr % w1) * a.I2 + lo2;
-    const long long y1 = y0 + w2 - 1;
+    const long long y0 = ((v.lo0 + rr / v.w1) * a.I1 + v.lo1 + rr % v.w1) * a.I2 + v.lo2;
+    const long long y1 = y0 + v.w2 - 1;
     for (long long b = y0 / EB; b <= y1 / EB; ++b) wave_block_key(cache, sel, a.n, b, w.bval, w.bidx);
   }
   __syncthreads();
   for (long long rr = wave; rr < nrow; rr += SEL_THREADS / 64) {
-    const long long y0 = ((lo0 + rr / w1) * a.I1 + lo1 + rr % w1) * a.I2 + lo2;
-    const long long y1 = y0 + w2 - 1;
+    const long long y0 = ((v.lo0 + rr / v.w1) * a.I1 + v.lo1 + rr % v.w1) * a.I2 + v.lo2;
+    const long long y1 = y0 + v.w2 - 1;
     for (long long sb = y0 / EB / ESB; sb <= y1 / EB / ESB; ++sb)
       wave_super_key(w.bval, w.bidx, nblk, sb, w.sval, w.sidx);
   }
@@ -574,19 +988,34 @@ EArgs make_eargs(const double* X, int64_t I0, int64_t I1, int64_t I2, double amp
   return a;
 }
 
+template <class F>
+int dispatch_kind(int kind, F&& f) {
+  switch (kind) {
+    case VGPOSP_KERNEL_EQ: return f(std::integral_constant<int, VGPOSP_KERNEL_EQ>{});
+    case VGPOSP_KERNEL_MATERN12: return f(std::integral_constant<int, VGPOSP_KERNEL_MATERN12>{});
+    case VGPOSP_KERNEL_MATERN32: return f(std::integral_constant<int, VGPOSP_KERNEL_MATERN32>{});
+    default: return f(std::integral_constant<int, VGPOSP_KERNEL_MATERN52>{});
+  }
+}
+
 template <int KIND>
 int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned char* sel,
-                    const ExactWS& w, hipStream_t s) {
+                    const ExactWS& w, int flags, hipStream_t s) {
   const long long n = a.n;
   const long long nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
+  const bool bounded = (flags & 1) != 0;
   VG_HIP(vg_memset(sel, 0, n, s));
-  hipLaunchKernelGGL(exact_coef_kernel<KIND>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, a,
-                     w.coef);
-  VG_LAUNCH_CHECK();
+  VG_HIP(vg_memset(w.lastA, 0, n, s));
+  VG_HIP(vg_memset(w.qexact, bounded ? 0 : 1, n, s));
+  if (!bounded) {
+    hipLaunchKernelGGL(exact_coef_kernel<KIND>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                       a, w.coef);
+    VG_LAUNCH_CHECK();
+  }
   {
     ProfScope ps("exact_score", s, 0.0, 16.0 * n);
     hipLaunchKernelGGL(exact_score_kernel<KIND>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
-                       a, qdiag, cache);
+                       a, qdiag, w.qexact, cache);
     VG_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(exact_block_keys_kernel, dim3((unsigned)ceil_div(nblk, 4)), dim3(256), 0, s,
@@ -594,6 +1023,48 @@ int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned
   VG_LAUNCH_CHECK();
   hipLaunchKernelGGL(exact_super_keys_kernel, dim3((unsigned)ceil_div(nsb, 4)), dim3(256), 0, s,
                      w.bval, w.bidx, nblk, w.sval, w.sidx, nsb);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+// cg_iters CG iterations for the column of *center into slot `slot`, from a fresh start.
+int exact_cg_run(const EArgs& a, const ExactWS& w, int slot, const long long* center, int radius,
+                 int cg_iters, double cg_tol, double* x, hipStream_t s) {
+  const long long bv = w.b0 * w.b1 * w.b2;
+  const int m = a.m1 + 1;
+  ProfScope ps("exact_cg", s, 0.0, (double)cg_iters * 8.0 * bv * (m + 9));
+  hipLaunchKernelGGL(exact_cg_start_kernel, dim3((unsigned)std::min<long long>(ceil_div(bv, 256), 1024)),
+                     dim3(256), 0, s, w, a.I0, a.I1, a.I2, slot, center, x);
+  VG_LAUNCH_CHECK();
+  const double tol2 = cg_tol * cg_tol;
+  const unsigned blocks = (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(bv, CG_T));
+  for (int it = 0; it < cg_iters; ++it) {
+    hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I0, a.I1, a.I2,
+                       a.offs, a.m1, radius, slot, center, it, (int)blocks, tol2);
+    VG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I1, a.I2, radius,
+                       slot, center, it, x);
+    VG_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+template <int KIND>
+int exact_update_t(const EArgs& a, const double* qdiag, double* cache, unsigned char* sel,
+                   const ExactWS& w, int round, const long long* picks, hipStream_t s) {
+  const long long nblk = ceil_div(a.n, EB);
+  ProfScope ps("exact_update", s, 0.0, 0.0);
+  hipLaunchKernelGGL(exact_rows_kernel<KIND>, dim3(1), dim3(128), 0, s, a, w, round, picks);
+  VG_LAUNCH_CHECK();
+  const long long side = 2LL * a.cutoff;
+  const long long nw = side * side * side;
+  if (nw > 0) {
+    hipLaunchKernelGGL(exact_window_kernel<KIND>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, s,
+                       a, qdiag, cache, sel, w, round, picks);
+    VG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(exact_window_keys_kernel, dim3(1), dim3(SEL_THREADS), 0, s, a, cache, sel, w,
+                     nblk, round, picks);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -606,12 +1077,6 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
   const long long nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
   const long long bv = w.b0 * w.b1 * w.b2;
   double* x = last ? nullptr : w.Qcols + (size_t)round * bv;
-  if (x) {
-    VG_HIP(vg_memset(w.r, 0, 8 * (size_t)bv, s));
-    VG_HIP(vg_memset(w.p0, 0, 8 * (size_t)bv, s));
-    VG_HIP(vg_memset(w.p1, 0, 8 * (size_t)bv, s));
-    VG_HIP(vg_memset(x, 0, 8 * (size_t)bv, s));
-  }
   {
     ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
     hipLaunchKernelGGL(exact_select_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, sel, a.I0, a.I1,
@@ -619,32 +1084,42 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
     VG_LAUNCH_CHECK();
   }
   if (!x) return 0;
-  {
-    const int m = a.m1 + 1;
-    ProfScope ps("exact_cg", s, 0.0, (double)cg_iters * 8.0 * bv * (m + 9));
-    const double tol2 = cg_tol * cg_tol;
-    const unsigned blocks = (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(bv, CG_T));
-    for (int it = 0; it < cg_iters; ++it) {
-      hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I0, a.I1, a.I2,
-                         a.offs, a.m1, radius, round, picks, it, tol2);
-      VG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I1, a.I2, radius,
-                         round, picks, it, x);
-      VG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(exact_cg_c_kernel, dim3(1), dim3(CG_T), 0, s, w, it, (int)blocks);
-      VG_LAUNCH_CHECK();
-    }
-  }
-  {
-    ProfScope ps("exact_update", s, 0.0, 0.0);
-    hipLaunchKernelGGL(exact_update_kernel<KIND>, dim3(1), dim3(SEL_THREADS), 0, s, a, qdiag, cache,
-                       sel, w, nblk, round, picks);
-    VG_LAUNCH_CHECK();
-  }
+  if (int rc = exact_cg_run(a, w, round, picks + round, radius, cg_iters, cg_tol, x, s)) return rc;
+  return exact_update_t<KIND>(a, qdiag, cache, sel, w, round, picks, s);
+}
+
+template <int KIND>
+int exact_refine_t(const EArgs& a, double* qdiag, double* cache, unsigned char* sel,
+                   const ExactWS& w, int slot, const long long* picks, int radius, int cg_iters,
+                   double cg_tol, hipStream_t s) {
+  const long long nblk = ceil_div(a.n, EB);
+  double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
+  if (int rc = exact_cg_run(a, w, slot, w.cand, radius, cg_iters, cg_tol, x, s)) return rc;
+  hipLaunchKernelGGL(exact_refine_end_kernel<KIND>, dim3(1), dim3(64), 0, s, a, qdiag, cache, sel, w,
+                     nblk, slot, picks);
+  VG_LAUNCH_CHECK();
   return 0;
 }
 
 }  // namespace
+
+#define VGPOSP_EXACT_PARAMS                                                                      \
+  int kind, const double *X, int64_t I0, int64_t I1, int64_t I2, double amp, double ls,          \
+      double diag_shift, double jitter, double threshold, const int *offsets, int m,             \
+      const double *tau, int ntau, int kmax, int cutoff, int radius, int cg_iters,               \
+      const double *qdiag, double *cache, uint8_t *selected, void *ws, size_t ws_bytes
+
+#define VGPOSP_EXACT_PROLOGUE(NAME)                                                              \
+  clear_error();                                                                                 \
+  VGPOSP_EXACT_CHECK_COMMON();                                                                   \
+  const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);           \
+  if (ws_bytes < w.bytes) {                                                                      \
+    set_error(NAME ": workspace %zu < %zu bytes", ws_bytes, w.bytes);                            \
+    return VGPOSP_E_WS;                                                                          \
+  }                                                                                              \
+  const EArgs a = make_eargs(X, I0, I1, I2, amp, ls, diag_shift, jitter, threshold, offsets, m, \
+                             tau, ntau, kmax, cutoff);                                           \
+  hipStream_t s = as_stream(stream)
 
 extern "C" size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
                                                int radius, int cg_iters) {
@@ -652,71 +1127,143 @@ extern "C" size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I
   return exact_layout(nullptr, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters).bytes;
 }
 
-extern "C" int vgposp_exact_prepare(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2,
-                                    double amp, double ls, double diag_shift, double jitter,
-                                    double threshold, const int* offsets, int m, const double* tau,
-                                    int ntau, int kmax, int cutoff, int radius, int cg_iters,
-                                    const double* qdiag, double* cache, uint8_t* selected, void* ws,
-                                    size_t ws_bytes, void* stream) {
-  clear_error();
-  VGPOSP_EXACT_CHECK_COMMON();
-  const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);
-  if (ws_bytes < w.bytes) {
-    set_error("vgposp_exact_prepare: workspace %zu < %zu bytes", ws_bytes, w.bytes);
-    return VGPOSP_E_WS;
-  }
-  const EArgs a = make_eargs(X, I0, I1, I2, amp, ls, diag_shift, jitter, threshold, offsets, m, tau,
-                             ntau, kmax, cutoff);
-  hipStream_t s = as_stream(stream);
-  switch (kind) {
-    case VGPOSP_KERNEL_EQ: return exact_prepare_t<VGPOSP_KERNEL_EQ>(a, qdiag, cache, selected, w, s);
-    case VGPOSP_KERNEL_MATERN12: return exact_prepare_t<VGPOSP_KERNEL_MATERN12>(a, qdiag, cache, selected, w, s);
-    case VGPOSP_KERNEL_MATERN32: return exact_prepare_t<VGPOSP_KERNEL_MATERN32>(a, qdiag, cache, selected, w, s);
-    default: return exact_prepare_t<VGPOSP_KERNEL_MATERN52>(a, qdiag, cache, selected, w, s);
-  }
+extern "C" int vgposp_exact_prepare(VGPOSP_EXACT_PARAMS, int flags, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_prepare");
+  VG_CHECK_ARG(flags == 0 || flags == 1, 24);
+  return dispatch_kind(kind, [&](auto K) {
+    return exact_prepare_t<decltype(K)::value>(a, qdiag, cache, selected, w, flags, s);
+  });
 }
 
-extern "C" int vgposp_exact_round(int kind, const double* X, int64_t I0, int64_t I1, int64_t I2,
-                                  double amp, double ls, double diag_shift, double jitter,
-                                  double threshold, const int* offsets, int m, const double* tau,
-                                  int ntau, int kmax, int cutoff, int radius, int cg_iters,
-                                  const double* qdiag, double* cache, uint8_t* selected, void* ws,
-                                  size_t ws_bytes, int round, int last, int64_t* picks,
+extern "C" int vgposp_exact_round(VGPOSP_EXACT_PARAMS, int round, int last, int64_t* picks,
                                   double* pick_delta, double cg_tol, void* stream) {
-  clear_error();
-  VGPOSP_EXACT_CHECK_COMMON();
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_round");
   VG_CHECK_ARG(round >= 0 && round < kmax, 24);
   VG_CHECK_ARG(picks != nullptr, 26);
   VG_CHECK_ARG(cg_tol >= 0.0, 28);
-  const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);
-  if (ws_bytes < w.bytes) {
-    set_error("vgposp_exact_round: workspace %zu < %zu bytes", ws_bytes, w.bytes);
-    return VGPOSP_E_WS;
-  }
-  const EArgs a = make_eargs(X, I0, I1, I2, amp, ls, diag_shift, jitter, threshold, offsets, m, tau,
-                             ntau, kmax, cutoff);
-  hipStream_t s = as_stream(stream);
   long long* pk = reinterpret_cast<long long*>(picks);
-  switch (kind) {
-    case VGPOSP_KERNEL_EQ:
-      return exact_round_t<VGPOSP_KERNEL_EQ>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
-    case VGPOSP_KERNEL_MATERN12:
-      return exact_round_t<VGPOSP_KERNEL_MATERN12>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
-    case VGPOSP_KERNEL_MATERN32:
-      return exact_round_t<VGPOSP_KERNEL_MATERN32>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
-    default:
-      return exact_round_t<VGPOSP_KERNEL_MATERN52>(a, qdiag, cache, selected, w, round, last, pk, pick_delta, radius, cg_iters, cg_tol, s);
+  return dispatch_kind(kind, [&](auto K) {
+    return exact_round_t<decltype(K)::value>(a, qdiag, cache, selected, w, round, last, pk,
+                                             pick_delta, radius, cg_iters, cg_tol, s);
+  });
+}
+
+extern "C" int vgposp_exact_coef(VGPOSP_EXACT_PARAMS, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_coef");
+  const long long n = a.n;
+  const int rc = dispatch_kind(kind, [&](auto K) {
+    hipLaunchKernelGGL(exact_coef_kernel<decltype(K)::value>, dim3((unsigned)ceil_div(n, 256)),
+                       dim3(256), 0, s, a, w.coef);
+    VG_LAUNCH_CHECK();
+    return 0;
+  });
+  if (rc) return rc;
+  const unsigned blocks = (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(n, 256));
+  hipLaunchKernelGGL(exact_gersh_kernel, dim3(blocks), dim3(256), 0, s, w.coef, n, m, w.gersh);
+  VG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(exact_gersh_final_kernel, dim3(1), dim3(64), 0, s, w.gersh, (int)blocks);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, const int* tab_nb,
+                                   const int* tab_cnt, int T, int K, double hi_scale, int64_t c0,
+                                   int64_t c1, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_bounds");
+  VG_CHECK_ARG(tab_off != nullptr, 24);
+  VG_CHECK_ARG(m == 1 || tab_nb != nullptr, 25);
+  VG_CHECK_ARG(tab_cnt != nullptr, 26);
+  VG_CHECK_ARG(T >= 1 && T <= BND_TMAX && (int64_t)T * (m - 1) <= BND_NBMAX, 27);
+  VG_CHECK_ARG(K >= 1 && K <= 4 * BND_SMAX, 28);
+  VG_CHECK_ARG(hi_scale >= 1.0, 29);
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= a.n, 30);
+  VG_CHECK_ARG(a.n < (1LL << 31), 3);
+  if (c1 == c0) return 0;
+  ProfScope ps("exact_bounds", s, 0.0, 0.0);
+  const long long waves = c1 - c0;
+  const unsigned blocks = (unsigned)std::min<long long>(ceil_div(waves, BND_WAVES), 65536);
+  double* out = const_cast<double*>(qdiag);
+  const long long lc0 = c0, lc1 = c1;
+#define VG_BOUNDS_REG(SMV)                                                                       \
+  if (T <= 64 * SMV) {                                                                           \
+    hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6>), dim3(blocks), dim3(BND_T), 0, s, w.coef, \
+                       a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, lc0, lc1, out); \
+    VG_LAUNCH_CHECK();                                                                           \
+    return 0;                                                                                    \
   }
+  if (a.m1 == 6) {  // the 7-point taper support of the reference's beta = 4
+    VG_BOUNDS_REG(1)
+    VG_BOUNDS_REG(2)
+    VG_BOUNDS_REG(3)
+    VG_BOUNDS_REG(4)
+    VG_BOUNDS_REG(6)
+    VG_BOUNDS_REG(9)
+  }
+#undef VG_BOUNDS_REG
+  hipLaunchKernelGGL(exact_bounds_kernel, dim3(blocks), dim3(BND_T), 0, s, w.coef, a.I0, a.I1, a.I2,
+                     a.m1, tab_off, tab_nb, tab_cnt, T, K, hi_scale, lc0, lc1, out);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_exact_argmax(VGPOSP_EXACT_PARAMS, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_argmax");
+  const long long nsb = ceil_div(ceil_div(a.n, EB), ESB);
+  ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
+  hipLaunchKernelGGL(exact_argmax_kernel, dim3(1), dim3(SEL_THREADS), 0, s, w, nsb);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_exact_refine(VGPOSP_EXACT_PARAMS, int slot, const int64_t* picks,
+                                   double cg_tol, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_refine");
+  VG_CHECK_ARG(slot >= 0 && slot < exact_slots(kmax), 24);
+  VG_CHECK_ARG(picks != nullptr, 25);
+  VG_CHECK_ARG(cg_tol >= 0.0, 26);
+  const long long* pk = reinterpret_cast<const long long*>(picks);
+  return dispatch_kind(kind, [&](auto K) {
+    return exact_refine_t<decltype(K)::value>(a, const_cast<double*>(qdiag), cache, selected, w,
+                                              slot, pk, radius, cg_iters, cg_tol, s);
+  });
+}
+
+extern "C" int vgposp_exact_pick(VGPOSP_EXACT_PARAMS, int round, int slot, int64_t* picks,
+                                 double* pick_delta, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_pick");
+  VG_CHECK_ARG(round >= 0 && round < kmax, 24);
+  VG_CHECK_ARG(slot >= 0 && slot < exact_slots(kmax), 25);
+  VG_CHECK_ARG(picks != nullptr, 26);
+  const long long nblk = ceil_div(a.n, EB);
+  hipLaunchKernelGGL(exact_pick_kernel, dim3(1), dim3(64), 0, s, cache, selected, a.n, w, nblk,
+                     round, slot, reinterpret_cast<long long*>(picks), pick_delta);
+  VG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vgposp_exact_update(VGPOSP_EXACT_PARAMS, int round, const int64_t* picks,
+                                   void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_update");
+  VG_CHECK_ARG(round >= 0 && round < kmax, 24);
+  VG_CHECK_ARG(picks != nullptr, 25);
+  const long long* pk = reinterpret_cast<const long long*>(picks);
+  return dispatch_kind(kind, [&](auto K) {
+    return exact_update_t<decltype(K)::value>(a, qdiag, cache, selected, w, round, pk, s);
+  });
 }
 
 extern "C" int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
                                     int radius, int cg_iters, double** qcols, int64_t** boxlo,
-                                    int** cgstate) {
+                                    int** cgstate, int** slot_of_round, int64_t** cand,
+                                    double** gersh) {
   clear_error();
   VG_CHECK_ARG(ws != nullptr, 1);
   const ExactWS w = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters);
   if (qcols) *qcols = w.Qcols;
   if (boxlo) *boxlo = reinterpret_cast<int64_t*>(w.boxlo);
   if (cgstate) *cgstate = w.cgstate;
+  if (slot_of_round) *slot_of_round = w.slot_of_round;
+  if (cand) *cand = reinterpret_cast<int64_t*>(w.cand);
+  if (gersh) *gersh = w.gersh;
   return 0;
 }

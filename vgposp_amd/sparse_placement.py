@@ -355,8 +355,79 @@ class FrontalSelectedInverse:
                 raise CholeskyError(bad[1], bad[0])
 
 
+def reach_table(offsets, K):
+    """The grid offsets within K stencil steps of a node (breadth-first over the stencil
+    ``offsets`` [m-1, 3]), sorted by step count, then C order: (tab [T, 3] int32 with the node
+    itself first, cnt [K + 1] int32 = offsets within d steps, nb [T, m-1] int32 = row of
+    tab[i] + offsets[o] in the table or -1).  The K-step Krylov space of e_y lives on exactly these
+    nodes (around y, clipped to the grid)."""
+    offs = [tuple(int(v) for v in o) for o in np.asarray(offsets, dtype=np.int64).reshape(-1, 3)]
+    dist = {(0, 0, 0): 0}
+    frontier = [(0, 0, 0)]
+    for d in range(1, int(K) + 1):
+        nxt = []
+        for v in frontier:
+            for o in offs:
+                w = (v[0] + o[0], v[1] + o[1], v[2] + o[2])
+                if w not in dist:
+                    dist[w] = d
+                    nxt.append(w)
+        frontier = nxt
+    items = sorted(dist.items(), key=lambda kv: (kv[1], kv[0]))
+    tab = np.array([k for k, _ in items], dtype=np.int32).reshape(-1, 3)
+    dd = np.array([v for _, v in items], dtype=np.int64)
+    cnt = np.array([(dd <= d).sum() for d in range(int(K) + 1)], dtype=np.int32)
+    pos = {k: i for i, (k, _) in enumerate(items)}
+    nb = np.full((len(tab), max(len(offs), 1)), -1, dtype=np.int32)
+    for i, (k, _) in enumerate(items):
+        for j, o in enumerate(offs):
+            nb[i, j] = pos.get((k[0] + o[0], k[1] + o[1], k[2] + o[2]), -1)
+    return tab, cnt, nb[:, :len(offs)]
+
+
+def cg_iterations_for(lam_min, lam_max, tol=1e-16):
+    """CG iterations for a relative residual of ``tol`` on a spectrum inside [lam_min, lam_max]
+    (the Chebyshev bound 2 rho^it, plus 4 for rounding)."""
+    kappa = lam_max / lam_min
+    rho = (math.sqrt(kappa) - 1) / (math.sqrt(kappa) + 1)
+    if rho <= 0:
+        return 1
+    return int(min(400, math.ceil(math.log(tol / 2) / math.log(rho)) + 4))
+
+
+BOUND_TMAX, BOUND_NBMAX = 14 * 64, 8192     # exact_bounds_kernel's register / LDS tables
+BOUND_MARGIN = 1e-12                       # relative rounding margin on the upper bounds
+
+
+def bound_steps(offsets, lam_min, lam_max, target=1e-6, kmax=12):
+    """(K, hi_scale, width) for vgposp_exact_bounds: the fewest CG steps whose bracket width
+    4 rho^2K is <= target, else the most whose reach table fits the kernel (at most kmax);
+    rho = (sqrt(kappa) - 1) / (sqrt(kappa) + 1) from the Gershgorin bounds.  The bracket only
+    decides how often the rounds refine (a CG column each): at 128^3, beta = 4 a width of 1e-6
+    (K = 5) refines 51 times for k = 50, 2e-5 (K = 4) 111 times, 4e-8 (K = 6) 50 times at twice
+    the bounds cost.  None when the bounds cannot bracket Q_yy (lambda_min <= 0, or no K with
+    4 rho^2K < 1/2)."""
+    if not (lam_min > 0.0 and lam_max >= lam_min):
+        return None
+    kappa = lam_max / lam_min
+    rho = (math.sqrt(kappa) - 1.0) / (math.sqrt(kappa) + 1.0)
+    m1 = len(np.asarray(offsets).reshape(-1, 3))
+    best = None
+    for K in range(1, kmax + 1):
+        tab, _, _ = reach_table(offsets, K)
+        if len(tab) > BOUND_TMAX or len(tab) * m1 > BOUND_NBMAX:
+            break
+        width = 4.0 * rho ** (2 * K)
+        if width < 0.5:
+            best = (K, (1.0 + BOUND_MARGIN) / (1.0 - width), width)
+            if width <= target:
+                break
+    return best
+
+
 class ExactWindowGreedy:
-    """The rounds of algorithm 3 on a TaperProblem, given diag(Q)."""
+    """The rounds of algorithm 3 on a TaperProblem: given diag(Q) (``run``, after the selected
+    inverse), or with diag(Q) only bounded (``run_bounded``, after ``bound_qdiag``)."""
 
     def __init__(self, prob: TaperProblem, kmax, cutoff, cg_tol=1e-16, cg_iters=None):
         if kmax > 128:
@@ -375,6 +446,9 @@ class ExactWindowGreedy:
         self.box = [min(2 * self.radius * self.cg_iters + 1, s) for s in prob.shape]
         self.ws = torch.empty(query("vgposp_exact_workspace_bytes", *prob.shape, prob.m, self.kmax,
                                     self.radius, self.cg_iters), dtype=torch.uint8, device=dev)
+        self.nslots = 2 * self.kmax
+        self.refinements = 0
+        self.bound = None
 
     def _args(self, qdiag):
         pr = self.p
@@ -388,7 +462,7 @@ class ExactWindowGreedy:
         if k > self.kmax:
             raise ValueError(f"k = {k} > kmax = {self.kmax}")
         self.picks.fill_(-1)
-        call("vgposp_exact_prepare", *self._args(qdiag), _stream())
+        call("vgposp_exact_prepare", *self._args(qdiag), 0, _stream())
         if snapshots is not None:
             snapshots.append(self.cache.clone())
         for t in range(k):
@@ -399,60 +473,200 @@ class ExactWindowGreedy:
                 snapshots.append(self.cache.clone())
         return self.picks[:k]
 
+    # ---------------------------------------------------------------- bounded-lazy form
+    def gershgorin(self, qdiag):
+        """Stencil coefficients + Gershgorin [lambda_min, lambda_max] of Sigma + eps I (one host
+        read)."""
+        call("vgposp_exact_coef", *self._args(qdiag), _stream())
+        off = self._buffers()[5]
+        g = self.ws[off: off + 16].view(torch.float64).cpu()
+        return float(g[0]), float(g[1])
+
+    def bound_qdiag(self, qdiag, c0=0, c1=None, steps=None):
+        """qdiag[c0:c1] <- upper bounds of Q_yy (vgposp_exact_bounds).  Returns the (K, hi_scale,
+        width) used, or None when the spectrum bounds cannot bracket Q_yy (then the selected
+        inverse is the only exact route)."""
+        lo, hi = self.gershgorin(qdiag)
+        b = bound_steps(self.p.offs_np, lo, hi) if steps is None else steps
+        self.bound = b
+        if b is None:
+            return None
+        # the measured spectrum bounds are tighter than the kernel-agnostic one the columns were
+        # sized with: fewer CG iterations (and a smaller Krylov box) give the same tolerance
+        its = cg_iterations_for(lo, hi, self.cg_tol)
+        if its < self.cg_iters:
+            self.cg_iters = its
+            self.box = [min(2 * self.radius * its + 1, s) for s in self.p.shape]
+        K, scale, _ = b
+        tab, cnt, nb = reach_table(self.p.offs_np, K)
+        dev = self.p.device
+        self._tab = [torch.as_tensor(np.ascontiguousarray(a).reshape(-1), dtype=torch.int32,
+                                     device=dev) for a in (tab, nb if nb.size else np.zeros(1), cnt)]
+        c1 = self.p.n if c1 is None else int(c1)
+        call("vgposp_exact_bounds", *self._args(qdiag), _p(self._tab[0]), _p(self._tab[1]),
+             _p(self._tab[2]), len(tab), K, scale, int(c0), c1, _stream())
+        return b
+
+    def run_bounded(self, qdiag, k):
+        """The rounds with qdiag holding upper bounds of Q_yy: the cache holds upper bounds of the
+        reference's cached deltas; an arg-max that lands on a candidate whose Q_yy is only bounded
+        refines it (its CG column; its cache entry becomes the reference's value) and the arg-max
+        is taken again, so every pick is the reference's arg-max.  One host read per arg-max."""
+        if k > self.kmax:
+            raise ValueError(f"k = {k} > kmax = {self.kmax}")
+        self.picks.fill_(-1)
+        args = self._args(qdiag)
+        call("vgposp_exact_prepare", *args, 1, _stream())
+        cand_off = self._buffers()[4]
+        cand = self.ws[cand_off: cand_off + 8].view(torch.int64)
+        colslot, order, free = {}, [], list(range(self.nslots - 1, -1, -1))
+        self.refinements = 0
+        for t in range(k):
+            while True:
+                call("vgposp_exact_argmax", *args, _stream())
+                c = int(cand.item())
+                if c < 0 or c in colslot:
+                    break
+                if free:
+                    slot = free.pop()
+                else:  # recycle the oldest refined candidate that was not picked
+                    old = order.pop(0)
+                    slot = colslot.pop(old)
+                call("vgposp_exact_refine", *args, slot, _p(self.picks), self.cg_tol, _stream())
+                colslot[c] = slot
+                order.append(c)
+                self.refinements += 1
+            if c < 0:
+                break
+            slot = colslot[c]
+            order.remove(c)      # pinned: the pick's column is a row of Q_A
+            call("vgposp_exact_pick", *args, t, slot, _p(self.picks), _p(self.pick_delta),
+                 _stream())
+            if t < k - 1:
+                call("vgposp_exact_update", *args, t, _p(self.picks), _stream())
+        return self.picks[:k]
+
     def _buffers(self):
-        q, b, c = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        ptrs = [ctypes.c_void_p() for _ in range(6)]
         call("vgposp_exact_buffers", _p(self.ws), *self.p.shape, self.p.m, self.kmax, self.radius,
-             self.cg_iters, ctypes.byref(q), ctypes.byref(b), ctypes.byref(c))
+             self.cg_iters, *[ctypes.byref(q) for q in ptrs])
         base = self.ws.data_ptr()
-        return q.value - base, b.value - base, c.value - base
+        return [q.value - base for q in ptrs]
 
     def q_columns(self):
-        """The CG columns Q e_{a_t} expanded to the grid: [kmax, N] (zero outside each box)."""
-        qo, bo, _ = self._buffers()
+        """The CG columns Q e_{a_t} of the picks expanded to the grid: [kmax, N] (zero outside
+        each box; rows of picks without a column are zero)."""
+        qo, bo, _, so, _, _ = self._buffers()
         b0, b1, b2 = self.box
         bv = b0 * b1 * b2
-        cols = self.ws[qo: qo + 8 * self.kmax * bv].view(torch.float64).view(self.kmax, b0, b1, b2)
-        lo = self.ws[bo: bo + 8 * 3 * self.kmax].view(torch.int64).view(self.kmax, 3).cpu()
+        cols = self.ws[qo: qo + 8 * self.nslots * bv].view(torch.float64).view(self.nslots, b0, b1,
+                                                                               b2)
+        lo = self.ws[bo: bo + 8 * 3 * self.nslots].view(torch.int64).view(self.nslots, 3).cpu()
+        slots = self.ws[so: so + 4 * self.kmax].view(torch.int32).cpu()
+        picks = self.picks.cpu()
         full = torch.zeros((self.kmax,) + self.p.shape, dtype=torch.float64, device=self.ws.device)
         for t in range(self.kmax):
-            l0, l1, l2 = (int(v) for v in lo[t])
-            if not all(0 <= l <= s - b for l, s, b in zip((l0, l1, l2), self.p.shape, self.box)):
-                continue  # no column for this pick (the last one, or not placed)
-            full[t, l0:l0 + b0, l1:l1 + b1, l2:l2 + b2] = cols[t]
+            s = int(slots[t])
+            if int(picks[t]) < 0 or not 0 <= s < self.nslots:
+                continue
+            l0, l1, l2 = (int(v) for v in lo[s])
+            if not all(0 <= l <= sh - b for l, sh, b in zip((l0, l1, l2), self.p.shape, self.box)):
+                continue  # no column for this pick (the last one of the selected-inverse form)
+            full[t, l0:l0 + b0, l1:l1 + b1, l2:l2 + b2] = cols[s]
         return full.view(self.kmax, -1)
 
     def cg_iterations_used(self):
         """Iterations the last CG solve took (the full budget if it did not stop early)."""
-        _, _, co = self._buffers()
+        co = self._buffers()[2]
         st = self.ws[co: co + 8].view(torch.int32)
         return int(st[1]) if int(st[0]) else self.cg_iters
 
 
+def allgather_slabs(vec, group=None):
+    """Every rank computed vec[r chunk: (r + 1) chunk] (chunk = ceil(n / world)); afterwards
+    every rank holds all of it (one all-gather; gloo groups stage through the host)."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    n = vec.numel()
+    chunk = -(-n // world)
+    full = torch.zeros(chunk * world, dtype=vec.dtype, device=vec.device)
+    mine = torch.zeros(chunk, dtype=vec.dtype, device=vec.device)
+    lo, hi = min(rank * chunk, n), min((rank + 1) * chunk, n)
+    mine[:hi - lo] = vec[lo:hi]
+    if dist.get_backend(group) == "gloo" and vec.is_cuda:
+        out = full.cpu()
+        dist.all_gather_into_tensor(out, mine.cpu(), group=group)
+        full.copy_(out)
+    else:
+        dist.all_gather_into_tensor(full, mine, group=group)
+    vec.copy_(full[:n])
+    return 8 * chunk * (world - 1)
+
+
+def slab_of(n, world, rank):
+    chunk = -(-n // world)
+    return min(rank * chunk, n), min((rank + 1) * chunk, n)
+
+
 class ExactTaperPlacement:
-    """One C4 problem end to end: selected inverse + rounds (device-resident)."""
+    """One C4 problem end to end (device-resident).  method:
+      "bounds": upper bounds of diag(Q) from K-step CG per candidate (sharded over the ranks of
+                `group`, one all-gather) and the bounded-lazy rounds (replicated on every rank);
+      "selinv": diag(Q) from the multifrontal selected inverse (sharded subtree-to-subcube) and
+                the plain rounds — the only form that also yields delta_cached_iters;
+      "auto":   "bounds" unless snapshots are asked for or the spectrum bounds cannot bracket."""
 
     def __init__(self, X, shape, k, cutoff, beta=4.0, kind="eq", amp=1.0, ls=1.0, diag_shift=0.0,
-                 jitter=TF_JITTER, threshold=TF_SMALL, leaf=512, device=None, group=None):
+                 jitter=TF_JITTER, threshold=TF_SMALL, leaf=512, device=None, group=None,
+                 method="auto"):
+        if method not in ("auto", "bounds", "selinv"):
+            raise ValueError(f"method must be auto / bounds / selinv, got {method!r}")
         self.prob = TaperProblem(X, shape, beta, kind, amp, ls, diag_shift, jitter, threshold,
                                  device)
         import torch.distributed as dist
-        comm = FrontComm(group) if dist.is_initialized() and dist.get_world_size(group) > 1 \
-            else None
-        self.sel = FrontalSelectedInverse(self.prob, leaf, comm=comm)
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.comm = FrontComm(group) if self.world > 1 else None
+        self.leaf = leaf
+        self._sel = None
         self.greedy = ExactWindowGreedy(self.prob, k, cutoff)
         self.k = int(k)
+        self.method = method
+        self.used = None
+        self.exchanged_bytes = 0
         self.qdiag = torch.empty(self.prob.n, dtype=torch.float64, device=self.prob.device)
 
+    @property
+    def sel(self):
+        if self._sel is None:
+            self._sel = FrontalSelectedInverse(self.prob, self.leaf, comm=self.comm)
+        return self._sel
+
     def run(self, snapshots=None):
+        if self.method != "selinv" and snapshots is None:
+            c0, c1 = slab_of(self.prob.n, self.world, self.rank)
+            b = self.greedy.bound_qdiag(self.qdiag, c0, c1)
+            if b is not None:
+                if self.world > 1:
+                    self.exchanged_bytes = allgather_slabs(self.qdiag, self.group)
+                self.used = "bounds"
+                return self.greedy.run_bounded(self.qdiag, self.k)
+            if self.method == "bounds":
+                raise ValueError("the Gershgorin bounds of Sigma + eps I do not bracket Q_yy "
+                                 "(not diagonally dominant): use method='selinv'")
+        self.used = "selinv"
         self.sel.run(out=self.qdiag)
         return self.greedy.run(self.qdiag, self.k, snapshots)
 
     def check(self):
-        self.sel.check()
+        if self.used == "selinv":
+            self.sel.check()
 
 
 def tapered_placement_algorithm_3(X, k, COVER_spatial, cutoff, beta=4.0, kernel="eq", amp=1.0,
-                                  ls=1.0, diag_shift=0.0, snapshots=False, leaf=512, group=None):
+                                  ls=1.0, diag_shift=0.0, snapshots=False, leaf=512, group=None,
+                                  method="auto"):
     """snippets_a3.sparse_placement_algorithm_3(cov_vv, k, COVER_spatial, cutoff) for the tapered
     covariance of the grid points X (C order, COVER_spatial = (I0, I1, I2)), exact, without the
     dense cov_vv.  -> (picks as a list of np.int64 in selection order, the pick deltas,
@@ -462,7 +676,7 @@ def tapered_placement_algorithm_3(X, k, COVER_spatial, cutoff, beta=4.0, kernel=
     if len(X) != N:                                         # snippets_a3.py:51 tf.Assert
         raise ValueError(f"assertion failed: N = {len(X)} != prod(COVER_spatial) = {N}")
     run = ExactTaperPlacement(X, shape, k, cutoff, beta, kernel, amp, ls, diag_shift, leaf=leaf,
-                              group=group)
+                              group=group, method=method)
     snaps = [] if snapshots else None
     picks = run.run(snaps).cpu().numpy()
     run.check()
@@ -471,4 +685,5 @@ def tapered_placement_algorithm_3(X, k, COVER_spatial, cutoff, beta=4.0, kernel=
 
 
 __all__ = ["TaperProblem", "HipFrontalOps", "FrontComm", "FrontalSelectedInverse",
-           "ExactWindowGreedy", "ExactTaperPlacement", "tapered_placement_algorithm_3"]
+           "ExactWindowGreedy", "ExactTaperPlacement", "tapered_placement_algorithm_3",
+           "reach_table", "bound_steps", "allgather_slabs", "slab_of"]
