@@ -672,30 +672,36 @@ __device__ __forceinline__ void block_partial(double v, double* part, double* re
   }
 }
 
-// Box-local node l -> (grid coordinates, inside the active region of iteration it).  The
-// iterate's support after `it` steps lies within `it` stencil radii of the centre in every axis;
-// the kernels skip the rest of the box (its entries are and stay exactly zero).
-struct BoxNode {
-  long long g0, g1, g2;
-  bool active;
+// The active cube of CG iteration it: the nodes within (it + 1) stencil radii of the centre
+// (the iterate's support), inside the column's box.  Thread t of the launch handles cube node t.
+struct ActiveCube {
+  long long c0, c1, c2, e1, e2, ne;
+  long long lo0, lo1, lo2;
 };
 
-__device__ __forceinline__ BoxNode box_node(const ExactWS& w, long long l, const long long* lo,
-                                            long long a0, long long a1, long long a2,
-                                            long long rad) {
-  BoxNode b;
-  const long long l0 = l / (w.b1 * w.b2), l1 = (l / w.b2) % w.b1, l2 = l % w.b2;
-  b.g0 = lo[0] + l0;
-  b.g1 = lo[1] + l1;
-  b.g2 = lo[2] + l2;
-  b.active = llabs(b.g0 - a0) <= rad && llabs(b.g1 - a1) <= rad && llabs(b.g2 - a2) <= rad;
-  return b;
+__device__ __forceinline__ ActiveCube active_cube(const ExactWS& w, long long I1, long long I2,
+                                                  int slot, long long a, int it, int srad) {
+  ActiveCube q;
+  const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
+  q.lo0 = w.boxlo[3 * slot];
+  q.lo1 = w.boxlo[3 * slot + 1];
+  q.lo2 = w.boxlo[3 * slot + 2];
+  const long long rad = min((long long)(it + 1) * srad, w.H);
+  q.c0 = max(a0 - rad, q.lo0);
+  q.c1 = max(a1 - rad, q.lo1);
+  q.c2 = max(a2 - rad, q.lo2);
+  const long long e0 = min(a0 + rad, q.lo0 + w.b0 - 1) - q.c0 + 1;
+  q.e1 = min(a1 + rad, q.lo1 + w.b1 - 1) - q.c1 + 1;
+  q.e2 = min(a2 + rad, q.lo2 + w.b2 - 1) - q.c2 + 1;
+  q.ne = e0 * q.e1 * q.e2;
+  return q;
 }
 
 // CG iteration it, part A: beta from the last residual norms, p_it = r + beta p_{it-1} (computed
-// for the neighbours on the fly, written for this thread's own nodes), q = (S + eps I) p_it and
-// the partials of p_it . q.  Converged (|r|^2 <= tol2) -> every block returns; block 0 records it.
-// The solve is for the column of *center into slot `slot`.
+// for the neighbours on the fly, written for this thread's own node), q = (S + eps I) p_it and the
+// partials of p_it . q.  Converged (|r|^2 <= tol2) -> every block returns; block 0 records it.
+// The solve is for the column of *center into slot `slot`; the launch covers the active cube
+// (np_prev: the grid of the previous B launch, whose partials hold |r_it|^2).
 __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I0, long long I1,
                                                           long long I2, const int* offs, int m1,
                                                           int srad, int slot,
@@ -716,24 +722,22 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   const double beta = it == 0 ? 0.0 : rr / w.rr[it - 1];
   const double* pold = (it & 1) ? w.p0 : w.p1;  // p_{it-1}
   double* pnew = (it & 1) ? w.p1 : w.p0;        // p_it
-  const long long a = *center;
-  const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
-  const long long* lo = w.boxlo + 3 * slot;
-  const long long bv = w.b0 * w.b1 * w.b2;
-  const long long rad = min((long long)(it + 1) * srad, w.H);
+  const ActiveCube q = active_cube(w, I1, I2, slot, *center, it, srad);
   const int m = m1 + 1;
   double acc = 0.0;
-  for (long long l = (long long)blockIdx.x * CG_T + threadIdx.x; l < bv; l += (long long)CG_BLOCKS * CG_T) {
-    const BoxNode nd = box_node(w, l, lo, a0, a1, a2, rad);
-    if (!nd.active) continue;
+  for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
+       t += (long long)gridDim.x * CG_T) {
+    const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
+                    g2 = q.c2 + t % q.e2;
+    const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     const double pi = it == 0 ? w.r[l] : fma(beta, pold[l], w.r[l]);
-    const double* c = w.coef + ((nd.g0 * I1 + nd.g1) * I2 + nd.g2) * m;
+    const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * m;
     double s = c[0] * pi;
     for (int o = 0; o < m1; ++o) {
       const double cv = c[1 + o];
       if (cv == 0.0) continue;  // outside the grid
-      const long long j0 = nd.g0 + offs[3 * o] - lo[0], j1 = nd.g1 + offs[3 * o + 1] - lo[1],
-                      j2 = nd.g2 + offs[3 * o + 2] - lo[2];
+      const long long j0 = g0 + offs[3 * o] - q.lo0, j1 = g1 + offs[3 * o + 1] - q.lo1,
+                      j2 = g2 + offs[3 * o + 2] - q.lo2;
       if (j0 < 0 || j0 >= w.b0 || j1 < 0 || j1 >= w.b1 || j2 < 0 || j2 >= w.b2) continue;
       const long long j = (j0 * w.b1 + j1) * w.b2 + j2;
       const double pj = it == 0 ? w.r[j] : fma(beta, pold[j], w.r[j]);
@@ -746,7 +750,8 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   block_partial(acc, w.part_pq, red);
 }
 
-// CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2.
+// CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2
+// (same grid and cube as part A).
 __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I1, long long I2,
                                                           int srad, int slot,
                                                           const long long* center, int it,
@@ -756,14 +761,13 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
   const double pq = sum_partials(w.part_pq, (int)gridDim.x, red);  // the A kernel's grid
   const double alpha = w.rr[it] / pq;
   const double* p = (it & 1) ? w.p1 : w.p0;
-  const long long a = *center;
-  const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
-  const long long* lo = w.boxlo + 3 * slot;
-  const long long bv = w.b0 * w.b1 * w.b2;
-  const long long rad = min((long long)(it + 1) * srad, w.H);
+  const ActiveCube q = active_cube(w, I1, I2, slot, *center, it, srad);
   double acc = 0.0;
-  for (long long l = (long long)blockIdx.x * CG_T + threadIdx.x; l < bv; l += (long long)CG_BLOCKS * CG_T) {
-    if (!box_node(w, l, lo, a0, a1, a2, rad).active) continue;
+  for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
+       t += (long long)gridDim.x * CG_T) {
+    const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
+                    g2 = q.c2 + t % q.e2;
+    const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     x[l] = fma(alpha, p[l], x[l]);
     const double ri = fma(-alpha, w.q[l], w.r[l]);
     w.r[l] = ri;
@@ -1037,14 +1041,19 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int slot, const long long* ce
                      dim3(256), 0, s, w, a.I0, a.I1, a.I2, slot, center, x);
   VG_LAUNCH_CHECK();
   const double tol2 = cg_tol * cg_tol;
-  const unsigned blocks = (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(bv, CG_T));
+  unsigned prev = 1;
   for (int it = 0; it < cg_iters; ++it) {
+    // the unclipped active cube bounds the launch: a grid that grows with the iterate's support
+    const long long side = std::min<long long>(2LL * (it + 1) * radius + 1, 2 * w.H + 1);
+    const unsigned blocks =
+        (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(side * side * side, (long long)CG_T));
     hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I0, a.I1, a.I2,
-                       a.offs, a.m1, radius, slot, center, it, (int)blocks, tol2);
+                       a.offs, a.m1, radius, slot, center, it, (int)prev, tol2);
     VG_LAUNCH_CHECK();
     hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I1, a.I2, radius,
                        slot, center, it, x);
     VG_LAUNCH_CHECK();
+    prev = blocks;
   }
   return 0;
 }

@@ -498,13 +498,16 @@ class ExactWindowGreedy:
             self.cg_iters = its
             self.box = [min(2 * self.radius * its + 1, s) for s in self.p.shape]
         K, scale, _ = b
-        tab, cnt, nb = reach_table(self.p.offs_np, K)
-        dev = self.p.device
-        self._tab = [torch.as_tensor(np.ascontiguousarray(a).reshape(-1), dtype=torch.int32,
-                                     device=dev) for a in (tab, nb if nb.size else np.zeros(1), cnt)]
+        if getattr(self, "_tabK", None) != K:   # the reach tables, uploaded once per K
+            tab, cnt, nb = reach_table(self.p.offs_np, K)
+            dev = self.p.device
+            self._tab = [torch.as_tensor(np.ascontiguousarray(a).reshape(-1), dtype=torch.int32,
+                                         device=dev) for a in (tab, nb if nb.size else np.zeros(1),
+                                                               cnt)]
+            self._tabK, self._T = K, len(tab)
         c1 = self.p.n if c1 is None else int(c1)
         call("vgposp_exact_bounds", *self._args(qdiag), _p(self._tab[0]), _p(self._tab[1]),
-             _p(self._tab[2]), len(tab), K, scale, int(c0), c1, _stream())
+             _p(self._tab[2]), self._T, K, scale, int(c0), c1, _stream())
         return b
 
     def run_bounded(self, qdiag, k):
