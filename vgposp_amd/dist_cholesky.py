@@ -23,6 +23,12 @@ Every rank ends with the same L (the upper triangle of the buffer, Sigma, is nev
 all-gathers run on RCCL over device buffers ("nccl" backend), or through host staging on gloo (the
 CPU tests and the 2-ranks-on-one-GPU test).  At N = 65,536 and R = 8 they move ~26 GB in total
 (each rank receives 7/8 of it); the flops per rank drop ~7x.
+
+Overlap: the trailing update of a node is done in two parts.  Rows [0, h) of A22 (h = the split of
+the bottom-right child, the rows its top-left recursion factors first) are updated and
+all-gathered before that recursion starts; rows [h, n2) are updated next and their all-gather is
+issued asynchronously and only unpacked when an operation reads those rows (the child's panel), so
+it runs beside the child's whole top-left recursion.
 """
 from __future__ import annotations
 
@@ -50,11 +56,12 @@ def even_rows(n, world, align=ALIGN):
     return [(edges[r], edges[r + 1]) for r in range(world)]
 
 
-def lower_bands(n, world, align=ALIGN):
-    """[a, b) row bands of an n x n lower triangle with equal area: edge r at n sqrt(r / world)."""
-    edges = [0]
+def lower_bands(n, world, align=ALIGN, start=0):
+    """[a, b) row bands of rows [start, n) of an n x n lower triangle with equal area (row i has
+    i + 1 entries): edge r at sqrt(start^2 + (n^2 - start^2) r / world)."""
+    edges = [start]
     for r in range(1, world):
-        e = int(round(n * math.sqrt(r / world) / align)) * align
+        e = int(round(math.sqrt(start * start + (n * n - start * start) * r / world) / align)) * align
         edges.append(min(max(e, edges[-1]), n))
     edges.append(n)
     return [(edges[r], edges[r + 1]) for r in range(world)]
@@ -112,23 +119,38 @@ class DistCholesky:
         self.exchanged = 0  # doubles all-gathered (diagnostic)
 
     def factor(self):
+        self._pending = []
         self._rec(0, self.ops.n)
+        self._flush(0, self.ops.n)
+
+    def _splits(self, nsub):
+        return self.world > 1 and nsub >= self.dist_min and nsub > BLOCK_INV
 
     def _rec(self, col0, nsub):
         ops = self.ops
-        if self.world == 1 or nsub < self.dist_min or nsub <= BLOCK_INV:
+        if not self._splits(nsub):
+            self._flush(col0, col0 + nsub)
             ops.block(col0, nsub)
             return
         n1 = ops.split(nsub)
         n2 = nsub - n1
         base = col0 + n1
         self._rec(col0, n1)
+        self._flush(col0, col0 + nsub)     # the panel reads rows [col0, col0 + nsub)
         shares = even_rows(n2, self.world)
         ops.panel(col0, nsub, *shares[self.rank])
         self._exchange([(base + a, base + b, col0, base, 0) for a, b in shares])
-        bands = lower_bands(n2, self.world)
+        # trailing update: first the rows the bottom-right child factors first, then the rest
+        # with a deferred all-gather
+        h = ops.split(n2) if self._splits(n2) else n2
+        bands = lower_bands(h, self.world)
         ops.trailing(col0, nsub, *bands[self.rank])
         self._exchange([(base + a, base + b, base, base + b, 1) for a, b in bands])
+        if h < n2:
+            bands = lower_bands(n2, self.world, start=h)
+            ops.trailing(col0, nsub, *bands[self.rank])
+            self._exchange([(base + a, base + b, base, base + b, 1) for a, b in bands],
+                           defer=(base + h, base + n2))
         self._rec(base, n2)
 
     def _buf(self, key, numel, device):
@@ -138,28 +160,59 @@ class DistCholesky:
             self._bufs[key] = b
         return b[:numel]
 
-    def _exchange(self, pieces):
-        """All-gather every rank's piece (r0, r1, c0, c1, lower) of the matrix."""
+    def _exchange(self, pieces, defer=None):
+        """All-gather every rank's piece (r0, r1, c0, c1, lower) of the matrix.  ``defer`` = the
+        row range the pieces cover: the all-gather is issued asynchronously and the received
+        pieces are unpacked by the first _flush that touches those rows."""
         ops = self.ops
         sizes = [ops.pack_elems(*p) for p in pieces]
         S = max(sizes)
         if S == 0:
             return
-        send = self._buf("send", S, ops.device)
-        recv = self._buf("recv", self.world * S, ops.device)
+        if defer is None:
+            send = self._buf("send", S, ops.device)
+            recv = self._buf("recv", self.world * S, ops.device)
+        else:  # private buffers: they live until the unpack
+            send = torch.empty(S, dtype=torch.float64, device=ops.device)
+            recv = torch.empty(self.world * S, dtype=torch.float64, device=ops.device)
         if sizes[self.rank]:
             ops.pack(*pieces[self.rank], send, False)
+        host = None
         if self.staging:
             hs = send.cpu()
-            hr = torch.empty(self.world * S, dtype=torch.float64)
-            dist.all_gather_into_tensor(hr, hs, group=self.group)
-            recv.copy_(hr)
+            host = torch.empty(self.world * S, dtype=torch.float64)
+            work = dist.all_gather_into_tensor(host, hs, group=self.group,
+                                               async_op=defer is not None)
         else:
-            dist.all_gather_into_tensor(recv, send, group=self.group)
+            work = dist.all_gather_into_tensor(recv, send, group=self.group,
+                                               async_op=defer is not None)
+        entry = (defer, work, send, recv, host, pieces, sizes, S)
+        self.exchanged += sum(sizes)
+        if defer is None:
+            self._unpack(entry)
+        else:
+            self._pending.append(entry)
+
+    def _unpack(self, entry):
+        _, work, _, recv, host, pieces, sizes, S = entry
+        if work is not None:
+            work.wait()
+        if host is not None:
+            recv.copy_(host)
         for r, p in enumerate(pieces):
             if r != self.rank and sizes[r]:
-                ops.pack(*p, recv[r * S:r * S + sizes[r]], True)
-        self.exchanged += sum(sizes)
+                self.ops.pack(*p, recv[r * S:r * S + sizes[r]], True)
+
+    def _flush(self, r0, r1):
+        """Unpack (in issue order) every deferred all-gather whose rows meet [r0, r1)."""
+        keep = []
+        for e in getattr(self, "_pending", []):
+            a, b = e[0]
+            if a < r1 and r0 < b:
+                self._unpack(e)
+            else:
+                keep.append(e)
+        self._pending = keep
 
 
 def greedy_cholesky_ops(g):
