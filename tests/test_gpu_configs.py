@@ -62,7 +62,7 @@ def test_c2_assembly_and_potrf():
     torch.cuda.empty_cache()
 
 
-def _vgp_case(which, precision="fp64", kind="eq"):
+def _vgp_case(which, precision="fp64", kind="eq", rtol_loss=1e-8, rtol_grad=1e-6):
     from vgposp_amd import linalg
     from vgposp_amd.vgp_training import VGPObjective
     from vgposp_amd.workloads import vgp_c3_data, vgp_c5_data
@@ -78,11 +78,11 @@ def _vgp_case(which, precision="fp64", kind="eq"):
                                            linalg.as_device(X[bi]), linalg.as_device(y[bi]), B / N)
     got = (float(E), float(ga), float(gl), float(gs), gZ.cpu().numpy())
     ref = ogp.vgp_training_loss_grads(kind, Z, X, y, X[bi], y[bi], a, l, s, B / N)
-    assert got[0] == pytest.approx(ref[0], rel=1e-8)
+    assert got[0] == pytest.approx(ref[0], rel=rtol_loss)
     scale = max(abs(ref[1]), abs(ref[2]), abs(ref[3]), float(np.abs(ref[4]).max()))
     for g, r in zip(got[1:4], ref[1:4]):
-        assert abs(g - r) <= 1e-6 * scale, (g, r)
-    np.testing.assert_allclose(got[4], ref[4], rtol=0, atol=1e-6 * scale)
+        assert abs(g - r) <= rtol_grad * scale, (g, r)
+    np.testing.assert_allclose(got[4], ref[4], rtol=0, atol=rtol_grad * scale)
     return got
 
 
@@ -105,6 +105,15 @@ def test_c5_vgp_mixed_precision_vs_oracle(kind):
     """C5 as named: the M x M factorizations in fp32 + fp64 refinement (vgposp_potrf_mixed).  ELBO
     and gradients within the fp64 tolerances of the oracle (north_star asks 1e-5 relative)."""
     _vgp_case("c5", precision="mixed", kind=kind)
+
+
+@pytest.mark.timeout(400)
+def test_c5_vgp_mixed_two_steps_north_star_tolerance():
+    """The bench's C5 mixed line (MaternFiveHalves, the reference's arch-2 kernel): two fp64
+    refinement steps of the fp32 factor.  ELBO and gradients within north_star's 1e-5 of the fp64
+    oracle.  (The EQ Kzz of C5 is worse conditioned: after two steps its max|X A X^T - I| stays
+    above the 1e-6 the refinement accepts, so EQ keeps three.)"""
+    _vgp_case("c5", precision="mixed:2", kind="matern52", rtol_loss=1e-5, rtol_grad=1e-5)
 
 
 @pytest.mark.timeout(400)

@@ -34,7 +34,12 @@ def main():
     ap.add_argument("--shapes", action="store_true", help="per-shape GEMM / per-kernel dump")
     ap.add_argument("--c5", action="store_true", help="config C5: 65,536 x 5-D, M = 4^5, B = 8192")
     ap.add_argument("--mixed", action="store_true", help="fp32 Cholesky + fp64 refinement")
+    ap.add_argument("--kernel", default="eq")
+    ap.add_argument("--mixed-iters", type=int, default=None,
+                    help="fp64 refinement steps of the mixed factor (VGPOSP_MIXED_ITERS)")
     args = ap.parse_args()
+    if args.mixed_iters is not None:
+        os.environ["VGPOSP_MIXED_ITERS"] = str(args.mixed_iters)
     torch.cuda.set_device(0)
     if args.c5:
         X, y, Z = vgp_c5_data()
@@ -43,7 +48,8 @@ def main():
         X, y, Z = vgp_c3_data(args.n, args.m)
     N, B = len(X), args.batch
     train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B,
-                                          precision="mixed" if args.mixed else "fp64")
+                                          precision="mixed" if args.mixed else "fp64",
+                                          kernel=args.kernel)
     rng = np.random.default_rng(1)
     Xd = torch.as_tensor(X, device="cuda")
     yd = torch.as_tensor(y, device="cuda")
@@ -81,7 +87,9 @@ def main():
             print(f"{name:44s} {ms / args.steps:8.3f} ms/step {n / args.steps:6.1f} x {tf:6.1f} TF/s")
     _lib.prof_enable(False)
     M = Z.shape[0]
-    print(json.dumps({"N": N, "M": M, "batch": B, "ms_per_step": dt * 1e3, "graph": train_op.graph,
+    print(json.dumps({"N": N, "M": M, "batch": B, "kernel": args.kernel, "mixed": args.mixed,
+                      "mixed_iters": args.mixed_iters, "losses": losses[:3],
+                      "ms_per_step": dt * 1e3, "graph": train_op.graph,
                       "eager_profiled_ms_per_step": dt_eager * 1e3,
                       "elbo_steps_per_s": 1.0 / dt, "loss_first": losses[0], "loss_last": losses[-1],
                       "flops_2M2N_x2": 4.0 * M * M * N, "breakdown": prof}))

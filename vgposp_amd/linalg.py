@@ -7,6 +7,7 @@ contiguous, float64, on a ROCm device).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -201,11 +202,14 @@ def cholesky_(A, invert=False, check=True, ldiag=None):
     return A, ldiag, info
 
 
-def cholesky_inv_mixed(A, iters=3, check=True):
+def cholesky_inv_mixed(A, iters=None, check=True):
     """Mixed-precision inverse Cholesky factor of a full symmetric [n, n] A (config C5): fp32 factor
-    on the f32 matrix cores, ``iters`` fp64 refinement steps (vgposp_potrf_mixed).  Returns
+    on the f32 matrix cores, ``iters`` fp64 refinement steps (vgposp_potrf_mixed; default 3, or
+    the environment's VGPOSP_MIXED_ITERS for experiments).  Returns
     (L^-1 with zeros above the diagonal, diag(L) [n], info [1], resid [1] = max|X A X^T - I| of the
     last step); A is not modified."""
+    if iters is None:
+        iters = int(os.environ.get("VGPOSP_MIXED_ITERS", "3"))
     A = as_device(A)
     if A.dim() != 2 or A.shape[0] != A.shape[1]:
         raise ValueError("A must be square")

@@ -53,7 +53,7 @@ def kernel_vjp(kind, X1, X2, amp, ls, Kbar, u=None, w=None, want_x1bar=True):
     return grad, X1bar
 
 
-def _chol_inv(A, infos=None, mixed=False, inplace=False):
+def _chol_inv(A, infos=None, mixed=False, inplace=False, mixed_iters=None):
     """(L^-1 in the lower triangle, diag L [M]) of an SPD [M, M].  The upper triangle of the
     result is NOT zeroed: every consumer reads it as a stored-lower-triangular GEMM operand
     (tri_a / tri_b).  ``inplace`` factors A itself instead of a copy.  With ``infos`` (a list) the
@@ -61,7 +61,7 @@ def _chol_inv(A, infos=None, mixed=False, inplace=False):
     mixed=True: fp32 factor + fp64 refinement (linalg.cholesky_inv_mixed, config C5); the refined
     factor is the fp64 one to rounding."""
     if mixed:
-        Li, ld, info, _ = linalg.cholesky_inv_mixed(A, check=infos is None)
+        Li, ld, info, _ = linalg.cholesky_inv_mixed(A, iters=mixed_iters, check=infos is None)
     else:
         Li, ld, info = linalg.cholesky_(A if inplace else A.clone(), invert=True,
                                         check=infos is None)
@@ -123,9 +123,14 @@ class VGPObjective:
 
     def __init__(self, kind, X, y, jitter=1e-6, posterior_jitter=1e-6, trace_adjoint=False,
                  group=None, precision="fp64"):
-        if precision not in ("fp64", "mixed"):
-            raise ValueError(f"precision must be 'fp64' or 'mixed', got {precision!r}")
-        self.mixed = precision == "mixed"
+        # "mixed" = fp32 factor + 3 fp64 refinement steps (fp64 to rounding); "mixed:2" = two
+        # steps (|E| 1e-2 -> 1e-8: the ELBO within north_star's 1e-5 of fp64)
+        kind_, _, steps = str(precision).partition(":")
+        if kind_ not in ("fp64", "mixed") or (steps and (kind_ != "mixed" or not steps.isdigit())):
+            raise ValueError(f"precision must be 'fp64', 'mixed' or 'mixed:<steps>', "
+                             f"got {precision!r}")
+        self.mixed = kind_ == "mixed"
+        self.mixed_iters = int(steps) if steps else None
         self.kind = kind
         self.X = linalg.as_device(X)
         self.X = self.X[:, None] if self.X.dim() == 1 else self.X
@@ -191,7 +196,8 @@ class VGPObjective:
                 elif i == 1:  # computed on this stream: it depends only on s (before the fork)
                     A.diagonal().add_(s + 1e-6)
                 mine = []
-                Li, ld = _chol_inv(A, mine, self.mixed, inplace=True)
+                Li, ld = _chol_inv(A, mine, self.mixed, inplace=True,
+                                   mixed_iters=self.mixed_iters)
                 res.append((Li, ld, _spd_inv(Li), mine))
         (Lzi, _, Kzj_inv, i1), (Lpi, ldp, Kp_inv, i2), (Lki, ldk, Kzz_inv, i3) = res
         infos.extend(i1 + i2 + i3)
@@ -238,7 +244,8 @@ class VGPObjective:
             st.update(LiLi=spd[0], Lzi=F[1], Kzj_inv=spd[1], Lpi=F[2], ldp=ld[2], Kp_inv=spd[2],
                       Kzz_inv=spd[3], ldk=ld[3])
         else:
-            Li, lds = _chol_inv(F[0], infos, self.mixed, inplace=True)
+            Li, lds = _chol_inv(F[0], infos, self.mixed, inplace=True,
+                                mixed_iters=self.mixed_iters)
         t = linalg.gemm(Li, linalg.gemm(Li, _col(c), tri_a=True), transa=True, tri_a=True)
         m = linalg.gemm(Kzz, t).reshape(-1) / s
         A = linalg.gemm(Li, Kzz, tri_a=True)
