@@ -390,6 +390,7 @@ def c4_line(args, world, rank, barrier, maxtime):
            "exchanged_gb_per_step": (8.0 * (-(-run.prob.n // world)) * (world - 1) / 1e9
                                      if world > 1 else 0.0),
            "rounds_ms": rounds_ms, "refinements": g.refinements,
+           "refine_batches": g.refine_batches,
            "cg_iterations_per_column": g.cg_iters,
            "breakdown_ms": {n: v[0] for n, v in prof.items()}}
     # the selected-inverse form once: the same picks, and the fp64-MFMA rate of its fronts

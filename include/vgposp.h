@@ -539,12 +539,17 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  *     T <= 1024, T (m - 1) <= 8192.
  *   vgposp_exact_prepare(flags = 1): round 0 from those bounds (cache = upper bounds).
  *   vgposp_exact_argmax:  the arg-max candidate of the cache -> `cand` (vgposp_exact_buffers).
- *   vgposp_exact_refine:  Q e_cand by CG into column slot `slot` (< 2 kmax); Q_cc becomes exact and
- *     the candidate's cache entry the reference's value (scored with the A of its last re-score).
+ *   vgposp_exact_topb:    the B <= 8 best entries of the cache over V \ A, best first (the first is
+ *     the arg-max): out int64 [B + 1] (device) = count, candidates.
+ *   vgposp_exact_refine:  Q e_c for the nb <= 8 candidates cands[j] (device int64) by one batched
+ *     CG into column slots slots[j] (device int, < 2 kmax); each Q_cc becomes exact and the
+ *     candidate's cache entry the reference's value (scored with the A of its last re-score).
  *   vgposp_exact_pick:    cand (refined, column in `slot`) becomes pick `round`.
  *   vgposp_exact_update:  after pick `round`: the factor rows and the window re-score (upper
  *     bounds where Q_yy is still only bounded).
- *   The caller loops argmax -> (refine while the arg-max is not refined) -> pick -> update.
+ *   The caller loops top-B -> (refine the batch while the arg-max is not refined) -> pick ->
+ *   update: refining the B best entries together (one batched CG, the same launches as one column)
+ *   prepares the columns of the next rounds' picks, which are mostly among them.
  *
  *   vgposp_exact_buffers: device addresses of the column slots [2 kmax][b0 b1 b2] (box-local, C
  *     order, box dims b_d = min(2 radius cg_iters + 1, I_d)), their box origins int64
@@ -566,8 +571,9 @@ int vgposp_exact_bounds(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb
                         const int* tab_cnt, int T, int K, double hi_scale, int64_t c0, int64_t c1,
                         void* stream);
 int vgposp_exact_argmax(VGPOSP_EXACT_ARGS, void* stream);
-int vgposp_exact_refine(VGPOSP_EXACT_ARGS, int slot, const int64_t* picks, double cg_tol,
-                        void* stream);
+int vgposp_exact_refine(VGPOSP_EXACT_ARGS, int nb, const int64_t* cands, const int* slots,
+                        const int64_t* picks, double cg_tol, void* stream);
+int vgposp_exact_topb(VGPOSP_EXACT_ARGS, int B, int64_t* out, void* stream);
 int vgposp_exact_pick(VGPOSP_EXACT_ARGS, int round, int slot, int64_t* picks, double* pick_delta,
                       void* stream);
 int vgposp_exact_update(VGPOSP_EXACT_ARGS, int round, const int64_t* picks, void* stream);

@@ -16,6 +16,7 @@ from vgposp_amd.workloads import c4_grid  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 Ks = [int(v) for v in sys.argv[3:]] or [0]
+BATCH = int(os.environ.get("C4_BATCH", "8"))
 X, shape, ls = c4_grid(n)
 run = ExactTaperPlacement(X, shape, k, 3, 4.0, ls=ls, diag_shift=0.01 + 1e-6, method="bounds")
 g = run.greedy
@@ -33,12 +34,12 @@ for K in Ks:
         b = g.bound_qdiag(run.qdiag, steps=steps)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        picks = g.run_bounded(run.qdiag, k)
+        picks = g.run_bounded(run.qdiag, k, batch=BATCH)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
     _lib.prof_enable(True)
     g.bound_qdiag(run.qdiag, steps=steps)
-    g.run_bounded(run.qdiag, k)
+    g.run_bounded(run.qdiag, k, batch=BATCH)
     torch.cuda.synchronize()
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
@@ -46,6 +47,7 @@ for K in Ks:
     print(json.dumps({"n": n, "k": k, "K": b[0], "width": b[2], "gersh": [lo, hi],
                       "bounds_ms": (t1 - t0) * 1e3, "rounds_ms": (t2 - t1) * 1e3,
                       "total_ms": (t2 - t0) * 1e3, "placements_per_s": k / (t2 - t0),
-                      "refinements": g.refinements, "matches_fixture": (p == want) if want else None,
+                      "refinements": g.refinements, "batches": g.refine_batches,
+                      "matches_fixture": (p == want) if want else None,
                       "picks_head": p[:6],
                       "prof_ms": {kk: round(v[0], 3) for kk, v in prof.items()}}), flush=True)

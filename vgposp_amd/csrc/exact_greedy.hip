@@ -56,16 +56,16 @@ struct ExactWS {
   // CG on the box of half-width H around the pick (clipped into the grid): the Krylov vectors of
   // a solve of S e_a are exactly zero beyond H = iterations x stencil radius, so the box holds
   // every non-zero of the full-grid iteration.  Box-local vectors, [bv] each.
-  double* r;          // residual
-  double* p0;         // directions (two, alternating)
+  double* r;          // [CG_B][bv] residual (one vector per column of a batch)
+  double* p0;         // [CG_B][bv] directions (two, alternating)
   double* p1;
-  double* q;          // A p
+  double* q;          // [CG_B][bv] A p
   long long* boxlo;   // [kmax][3] box origin of each pick's column
   long long b0, b1, b2, H;
-  double* part_pq;    // [CG_BLOCKS]
-  double* part_rr;    // [CG_BLOCKS]
-  double* rr;         // [maxit + 2] residual norms per iteration
-  int* cgstate;       // [4]: done flag, iterations of the last solve
+  double* part_pq;    // [CG_B][CG_BLOCKS]
+  double* part_rr;    // [CG_B][CG_BLOCKS]
+  double* rr;         // [CG_B][maxit + 2] residual norms per iteration
+  int* cgstate;       // [CG_B][4]: done flag, iterations of the last solve
   double* LS;         // [kmax][kmax] chol(S_AA + eps I)
   double* LQ;         // [kmax][kmax] chol(Q_AA)
   double* Qcols;      // [nslots][bv]: Q e_c on candidate c's box (zero outside it)
@@ -81,6 +81,7 @@ struct ExactWS {
 __host__ __device__ __forceinline__ int exact_slots(int kmax) { return 2 * kmax; }
 
 constexpr int CG_MAXIT = 512;
+constexpr int CG_B = 8;       // columns solved together by one batched CG (blockIdx.y)
 
 static size_t ealign(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -106,15 +107,15 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
   w.bidx = (long long*)take(8 * nblk);
   w.sval = (double*)take(8 * nsb);
   w.sidx = (long long*)take(8 * nsb);
-  w.r = (double*)take(8 * (size_t)bv);
-  w.p0 = (double*)take(8 * (size_t)bv);
-  w.p1 = (double*)take(8 * (size_t)bv);
-  w.q = (double*)take(8 * (size_t)bv);
+  w.r = (double*)take(8 * (size_t)bv * CG_B);
+  w.p0 = (double*)take(8 * (size_t)bv * CG_B);
+  w.p1 = (double*)take(8 * (size_t)bv * CG_B);
+  w.q = (double*)take(8 * (size_t)bv * CG_B);
   w.boxlo = (long long*)take(8 * 3 * (size_t)exact_slots(kmax));
-  w.part_pq = (double*)take(8 * CG_BLOCKS);
-  w.part_rr = (double*)take(8 * CG_BLOCKS);
-  w.rr = (double*)take(8 * (CG_MAXIT + 2));
-  w.cgstate = (int*)take(16);
+  w.part_pq = (double*)take(8 * CG_BLOCKS * CG_B);
+  w.part_rr = (double*)take(8 * CG_BLOCKS * CG_B);
+  w.rr = (double*)take(8 * (CG_MAXIT + 2) * CG_B);
+  w.cgstate = (int*)take(16 * CG_B);
   w.LS = (double*)take(8 * (size_t)kmax * kmax);
   w.LQ = (double*)take(8 * (size_t)kmax * kmax);
   w.Qcols = (double*)take(8 * (size_t)exact_slots(kmax) * bv);
@@ -608,15 +609,39 @@ __global__ __launch_bounds__(64) void exact_pick_kernel(double* cache, unsigned 
   if (a >= 0) wave_refresh_keys(cache, sel, w, n, nblk, a);
 }
 
-// Start the CG solve of S x = e_c (c = *center) into column slot `slot`: r, p0, p1 and the
-// column zeroed except r = e_c, the box [c - H, c + H] per axis shifted inside the grid ->
-// boxlo[slot], rr[0] = 1, CG state cleared (marked done when there is no candidate).
+// Column j of a batched CG solve: its vectors and scalars in the workspace.
+struct CGCol {
+  double *r, *p0, *p1, *q, *part_pq, *part_rr, *rr;
+  int* state;
+};
+
+__device__ __forceinline__ CGCol cg_col(const ExactWS& w, int j) {
+  const size_t bv = (size_t)(w.b0 * w.b1 * w.b2);
+  CGCol c;
+  c.r = w.r + j * bv;
+  c.p0 = w.p0 + j * bv;
+  c.p1 = w.p1 + j * bv;
+  c.q = w.q + j * bv;
+  c.part_pq = w.part_pq + (size_t)j * CG_BLOCKS;
+  c.part_rr = w.part_rr + (size_t)j * CG_BLOCKS;
+  c.rr = w.rr + (size_t)j * (CG_MAXIT + 2);
+  c.state = w.cgstate + 4 * j;
+  return c;
+}
+
+// Start the CG solves of S x_j = e_{c_j} (c_j = centers[j], j = blockIdx.y) into column slots
+// slots[j]: r, p0, p1 and the column zeroed except r = e_c, the box [c - H, c + H] per axis
+// shifted inside the grid -> boxlo[slot], rr[0] = 1, state cleared (done when there is no
+// candidate).
 __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long long I0, long long I1,
-                                                             long long I2, int slot,
-                                                             const long long* center,
-                                                             double* __restrict__ x) {
-  const long long c = *center;
+                                                             long long I2, const int* slots,
+                                                             const long long* centers) {
+  const int j = blockIdx.y;
+  const CGCol cc = cg_col(w, j);
+  const long long c = centers[j];
+  const int slot = slots[j];
   const long long bv = w.b0 * w.b1 * w.b2;
+  double* x = w.Qcols + (size_t)slot * bv;
   long long lc = -1;
   if (c >= 0) {
     const long long a0 = c / (I1 * I2), a1 = (c / I2) % I1, a2 = c % I2;
@@ -631,15 +656,15 @@ __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long lon
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    w.rr[0] = 1.0;
-    w.cgstate[0] = c >= 0 ? 0 : 1;
-    w.cgstate[1] = 0;
+    cc.rr[0] = 1.0;
+    cc.state[0] = c >= 0 ? 0 : 1;
+    cc.state[1] = 0;
   }
   for (long long l = (long long)blockIdx.x * 256 + threadIdx.x; l < bv;
        l += (long long)gridDim.x * 256) {
-    w.r[l] = l == lc ? 1.0 : 0.0;
-    w.p0[l] = 0.0;
-    w.p1[l] = 0.0;
+    cc.r[l] = l == lc ? 1.0 : 0.0;
+    cc.p0[l] = 0.0;
+    cc.p1[l] = 0.0;
     x[l] = 0.0;
   }
 }
@@ -697,32 +722,33 @@ __device__ __forceinline__ ActiveCube active_cube(const ExactWS& w, long long I1
   return q;
 }
 
-// CG iteration it, part A: beta from the last residual norms, p_it = r + beta p_{it-1} (computed
-// for the neighbours on the fly, written for this thread's own node), q = (S + eps I) p_it and the
-// partials of p_it . q.  Converged (|r|^2 <= tol2) -> every block returns; block 0 records it.
-// The solve is for the column of *center into slot `slot`; the launch covers the active cube
-// (np_prev: the grid of the previous B launch, whose partials hold |r_it|^2).
+// CG iteration it, part A, for column j = blockIdx.y of a batch: beta from the last residual
+// norms, p_it = r + beta p_{it-1} (computed for the neighbours on the fly, written for this
+// thread's own node), q = (S + eps I) p_it and the partials of p_it . q.  Converged
+// (|r|^2 <= tol2) -> every block of the column returns; block 0 records it.  The launch covers
+// the active cube (np_prev: the grid of the previous B launch, whose partials hold |r_it|^2).
 __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I0, long long I1,
                                                           long long I2, const int* offs, int m1,
-                                                          int srad, int slot,
-                                                          const long long* center, int it,
+                                                          int srad, const int* slots,
+                                                          const long long* centers, int it,
                                                           int np_prev, double tol2) {
   __shared__ double red[CG_T / 64];
-  if (w.cgstate[0]) return;
+  const CGCol cc = cg_col(w, blockIdx.y);
+  if (cc.state[0]) return;
   // |r_it|^2 from the B kernel's partials (every block sums them in the same order)
-  const double rr = it == 0 ? w.rr[0] : sum_partials(w.part_rr, np_prev, red);
-  if (it > 0 && blockIdx.x == 0 && threadIdx.x == 0) w.rr[it] = rr;
+  const double rr = it == 0 ? cc.rr[0] : sum_partials(cc.part_rr, np_prev, red);
+  if (it > 0 && blockIdx.x == 0 && threadIdx.x == 0) cc.rr[it] = rr;
   if (rr <= tol2) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      w.cgstate[0] = 1;
-      w.cgstate[1] = it;
+      cc.state[0] = 1;
+      cc.state[1] = it;
     }
     return;
   }
-  const double beta = it == 0 ? 0.0 : rr / w.rr[it - 1];
-  const double* pold = (it & 1) ? w.p0 : w.p1;  // p_{it-1}
-  double* pnew = (it & 1) ? w.p1 : w.p0;        // p_it
-  const ActiveCube q = active_cube(w, I1, I2, slot, *center, it, srad);
+  const double beta = it == 0 ? 0.0 : rr / cc.rr[it - 1];
+  const double* pold = (it & 1) ? cc.p0 : cc.p1;  // p_{it-1}
+  double* pnew = (it & 1) ? cc.p1 : cc.p0;        // p_it
+  const ActiveCube q = active_cube(w, I1, I2, slots[blockIdx.y], centers[blockIdx.y], it, srad);
   const int m = m1 + 1;
   double acc = 0.0;
   for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
@@ -730,7 +756,7 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
     const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
                     g2 = q.c2 + t % q.e2;
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
-    const double pi = it == 0 ? w.r[l] : fma(beta, pold[l], w.r[l]);
+    const double pi = it == 0 ? cc.r[l] : fma(beta, pold[l], cc.r[l]);
     const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * m;
     double s = c[0] * pi;
     for (int o = 0; o < m1; ++o) {
@@ -740,28 +766,30 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
                       j2 = g2 + offs[3 * o + 2] - q.lo2;
       if (j0 < 0 || j0 >= w.b0 || j1 < 0 || j1 >= w.b1 || j2 < 0 || j2 >= w.b2) continue;
       const long long j = (j0 * w.b1 + j1) * w.b2 + j2;
-      const double pj = it == 0 ? w.r[j] : fma(beta, pold[j], w.r[j]);
+      const double pj = it == 0 ? cc.r[j] : fma(beta, pold[j], cc.r[j]);
       s = fma(cv, pj, s);
     }
     pnew[l] = pi;
-    w.q[l] = s;
+    cc.q[l] = s;
     acc = fma(pi, s, acc);
   }
-  block_partial(acc, w.part_pq, red);
+  block_partial(acc, cc.part_pq, red);
 }
 
 // CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2
-// (same grid and cube as part A).
+// (same grid and cube as part A; x = the column slot's box vector).
 __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I1, long long I2,
-                                                          int srad, int slot,
-                                                          const long long* center, int it,
-                                                          double* __restrict__ x) {
+                                                          int srad, const int* slots,
+                                                          const long long* centers, int it) {
   __shared__ double red[CG_T / 64];
-  if (w.cgstate[0]) return;
-  const double pq = sum_partials(w.part_pq, (int)gridDim.x, red);  // the A kernel's grid
-  const double alpha = w.rr[it] / pq;
-  const double* p = (it & 1) ? w.p1 : w.p0;
-  const ActiveCube q = active_cube(w, I1, I2, slot, *center, it, srad);
+  const CGCol cc = cg_col(w, blockIdx.y);
+  if (cc.state[0]) return;
+  const double pq = sum_partials(cc.part_pq, (int)gridDim.x, red);  // the A kernel's grid
+  const double alpha = cc.rr[it] / pq;
+  const double* p = (it & 1) ? cc.p1 : cc.p0;
+  const int slot = slots[blockIdx.y];
+  double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
+  const ActiveCube q = active_cube(w, I1, I2, slot, centers[blockIdx.y], it, srad);
   double acc = 0.0;
   for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
        t += (long long)gridDim.x * CG_T) {
@@ -769,11 +797,131 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
                     g2 = q.c2 + t % q.e2;
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     x[l] = fma(alpha, p[l], x[l]);
-    const double ri = fma(-alpha, w.q[l], w.r[l]);
-    w.r[l] = ri;
+    const double ri = fma(-alpha, cc.q[l], cc.r[l]);
+    cc.r[l] = ri;
     acc = fma(ri, ri, acc);
   }
-  block_partial(acc, w.part_rr, red);
+  block_partial(acc, cc.part_rr, red);
+}
+
+// The B best keys (value, then lower index) of `cnt` candidates, one workgroup: B rounds of a
+// block arg-max, each excluding the keys already taken.  key(i) -> (value, index); ties cannot
+// reorder because key_gt is a strict total order on distinct indices.
+template <class KeyFn>
+__device__ int block_topb(int cnt, int B, KeyFn key, double* sv, long long* si, long long* out_idx,
+                          int* out_pos, unsigned char* taken) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int i = t; i < cnt; i += SEL_THREADS) taken[i] = 0;
+  __syncthreads();
+  int got = 0;
+  for (int b = 0; b < B; ++b) {
+    double v = 0.0;
+    long long idx = -1;
+    int pos = -1;
+    for (int i = t; i < cnt; i += SEL_THREADS) {
+      if (taken[i]) continue;
+      double kv;
+      long long ki;
+      key(i, kv, ki);
+      if (key_gt(kv, ki, v, idx)) {
+        v = kv;
+        idx = ki;
+        pos = i;
+      }
+    }
+    // reduce (value, index, position): position rides along with the winning index
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(v, o, 64);
+      const long long oi = __shfl_xor(idx, o, 64);
+      const int op = __shfl_xor(pos, o, 64);
+      if (key_gt(ov, oi, v, idx)) {
+        v = ov;
+        idx = oi;
+        pos = op;
+      }
+    }
+    if (lane == 0) {
+      sv[wave] = v;
+      si[wave] = idx;
+      out_pos[CG_B + wave] = pos;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double bv = 0.0;
+      long long bi = -1;
+      int bp = -1;
+      for (int k = 0; k < SEL_THREADS / 64; ++k)
+        if (key_gt(sv[k], si[k], bv, bi)) {
+          bv = sv[k];
+          bi = si[k];
+          bp = out_pos[CG_B + k];
+        }
+      out_idx[b] = bi;
+      out_pos[b] = bp;
+      if (bp >= 0) taken[bp] = 1;
+    }
+    __syncthreads();
+    if (out_idx[b] < 0) break;
+    ++got;
+  }
+  __syncthreads();
+  return got;
+}
+
+// The B best cache entries over V \ A (vgposp_exact_topb): the B best superblocks contain them,
+// the B best blocks of those contain them, so three small top-B passes in one workgroup find them.
+// out[0] = count, out[1 ..] = the candidates, best first (out[1] is the arg-max).
+__global__ __launch_bounds__(SEL_THREADS) void exact_topb_kernel(const double* cache,
+                                                                 const unsigned char* sel,
+                                                                 long long n, ExactWS w,
+                                                                 long long nblk, long long nsb,
+                                                                 int B, long long* out) {
+  __shared__ double sv[SEL_THREADS / 64];
+  __shared__ long long si[SEL_THREADS / 64];
+  __shared__ long long tidx[CG_B];
+  __shared__ int tpos[CG_B + SEL_THREADS / 64];
+  __shared__ long long sbs[CG_B], blks[CG_B];
+  __shared__ unsigned char taken[CG_B * EB > ESB * CG_B ? CG_B * EB : ESB * CG_B];
+  __shared__ int nsbk, nblkk;
+  // superblocks whose key is one of the B best (nsb may exceed the LDS flags: scan by key)
+  if (nsb <= (long long)sizeof(taken)) {
+    const int g = block_topb((int)nsb, B, [&](int i, double& v, long long& k) {
+      v = w.sval[i];
+      k = w.sidx[i];
+    }, sv, si, tidx, tpos, taken);
+    if (threadIdx.x == 0) {
+      nsbk = g;
+      for (int b = 0; b < g; ++b) sbs[b] = tpos[b];
+    }
+  } else if (threadIdx.x == 0) {
+    nsbk = 0;  // (the caller falls back to the arg-max alone)
+  }
+  __syncthreads();
+  const int ns = nsbk;
+  // blocks of those superblocks
+  const int g2 = block_topb(ns * ESB, B, [&](int i, double& v, long long& k) {
+    const long long b = sbs[i / ESB] * ESB + (i % ESB);
+    v = b < nblk ? w.bval[b] : 0.0;
+    k = b < nblk ? w.bidx[b] : -1;
+  }, sv, si, tidx, tpos, taken);
+  if (threadIdx.x == 0) {
+    nblkk = g2;
+    for (int b = 0; b < g2; ++b) blks[b] = sbs[tpos[b] / ESB] * ESB + (tpos[b] % ESB);
+  }
+  __syncthreads();
+  const int nbk = nblkk;
+  // entries of those blocks
+  const int g3 = block_topb(nbk * EB, B, [&](int i, double& v, long long& k) {
+    const long long y = blks[i / EB] * EB + (i % EB);
+    const bool ok = y < n && !sel[y];
+    v = ok ? cache[y] : 0.0;
+    k = ok ? y : -1;
+  }, sv, si, tidx, tpos, taken);
+  if (threadIdx.x == 0) {
+    out[0] = g3;
+    for (int b = 0; b < g3; ++b) out[1 + b] = tidx[b];
+  }
 }
 
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
@@ -825,25 +973,35 @@ __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const long long
   return delta_from(sigma_diag<KIND>(a) - ns, qyy - nq, exact, a.jitter, a.thr);
 }
 
-// Bounded-lazy path, after the CG column of cand[0] in slot `slot`: Q_cc is now known; the
-// candidate's cache entry becomes the reference's value (scored with the A of its last re-score)
-// and its keys are refreshed.  One wave.
+// Bounded-lazy path, after the CG columns of the batch (cands[j] in slots[j], j < nb): each Q_cc
+// is now known; the candidate's cache entry becomes the reference's value (scored with the A of
+// its last re-score) and its keys are refreshed.  One wave, the batch in order (two candidates may
+// share a key block).
 template <int KIND>
 __global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* qdiag,
                                                               double* cache, unsigned char* sel,
-                                                              ExactWS w, long long nblk, int slot,
+                                                              ExactWS w, long long nblk, int nb,
+                                                              const int* slots,
+                                                              const long long* cands,
                                                               const long long* picks) {
-  const long long c = w.cand[0];
-  if (c < 0) return;
-  const double qcc = qslot_at(w, slot, c, a.I1, a.I2);
-  const double d = wave_rescore<KIND>(a, w, picks, (int)w.lastA[c], c, qcc, true);
-  if (threadIdx.x == 0) {
-    qdiag[c] = qcc;
-    w.qexact[c] = 1;
-    cache[c] = d;
+  for (int j = 0; j < nb; ++j) {
+    const long long c = cands[j];
+    if (c < 0) continue;
+    const double qcc = qslot_at(w, slots[j], c, a.I1, a.I2);
+    const double d = wave_rescore<KIND>(a, w, picks, (int)w.lastA[c], c, qcc, true);
+    if (threadIdx.x == 0) {
+      qdiag[c] = qcc;
+      w.qexact[c] = 1;
+      cache[c] = d;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_refresh_keys(cache, sel, w, a.n, nblk, c);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  __syncthreads();
-  wave_refresh_keys(cache, sel, w, a.n, nblk, c);
 }
 
 // After q_t = Q e_{a_t}, part 1: row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I) (one wave
@@ -1031,14 +1189,17 @@ int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned
   return 0;
 }
 
-// cg_iters CG iterations for the column of *center into slot `slot`, from a fresh start.
-int exact_cg_run(const EArgs& a, const ExactWS& w, int slot, const long long* center, int radius,
-                 int cg_iters, double cg_tol, double* x, hipStream_t s) {
+// cg_iters CG iterations for the nb columns centers[j] -> slots[j] (device arrays), from a
+// fresh start, batched over blockIdx.y.
+int exact_cg_run(const EArgs& a, const ExactWS& w, int nb, const int* slots,
+                 const long long* centers, int radius, int cg_iters, double cg_tol,
+                 hipStream_t s) {
   const long long bv = w.b0 * w.b1 * w.b2;
   const int m = a.m1 + 1;
-  ProfScope ps("exact_cg", s, 0.0, (double)cg_iters * 8.0 * bv * (m + 9));
-  hipLaunchKernelGGL(exact_cg_start_kernel, dim3((unsigned)std::min<long long>(ceil_div(bv, 256), 1024)),
-                     dim3(256), 0, s, w, a.I0, a.I1, a.I2, slot, center, x);
+  ProfScope ps("exact_cg", s, 0.0, (double)nb * cg_iters * 8.0 * bv * (m + 9));
+  hipLaunchKernelGGL(exact_cg_start_kernel,
+                     dim3((unsigned)std::min<long long>(ceil_div(bv, 256), 1024), (unsigned)nb),
+                     dim3(256), 0, s, w, a.I0, a.I1, a.I2, slots, centers);
   VG_LAUNCH_CHECK();
   const double tol2 = cg_tol * cg_tol;
   unsigned prev = 1;
@@ -1047,11 +1208,11 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int slot, const long long* ce
     const long long side = std::min<long long>(2LL * (it + 1) * radius + 1, 2 * w.H + 1);
     const unsigned blocks =
         (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(side * side * side, (long long)CG_T));
-    hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I0, a.I1, a.I2,
-                       a.offs, a.m1, radius, slot, center, it, (int)prev, tol2);
+    hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w, a.I0,
+                       a.I1, a.I2, a.offs, a.m1, radius, slots, centers, it, (int)prev, tol2);
     VG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks), dim3(CG_T), 0, s, w, a.I1, a.I2, radius,
-                       slot, center, it, x);
+    hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w, a.I1,
+                       a.I2, radius, slots, centers, it);
     VG_LAUNCH_CHECK();
     prev = blocks;
   }
@@ -1084,28 +1245,28 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
                   int radius, int cg_iters, double cg_tol, hipStream_t s) {
   const long long n = a.n;
   const long long nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
-  const long long bv = w.b0 * w.b1 * w.b2;
-  double* x = last ? nullptr : w.Qcols + (size_t)round * bv;
   {
     ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
     hipLaunchKernelGGL(exact_select_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, sel, a.I0, a.I1,
-                       a.I2, w, nblk, nsb, round, picks, pick_delta, x != nullptr ? 1 : 0);
+                       a.I2, w, nblk, nsb, round, picks, pick_delta, last ? 0 : 1);
     VG_LAUNCH_CHECK();
   }
-  if (!x) return 0;
-  if (int rc = exact_cg_run(a, w, round, picks + round, radius, cg_iters, cg_tol, x, s)) return rc;
+  if (last) return 0;
+  // the pick's column into slot `round` (exact_select_kernel wrote slot_of_round[round] = round)
+  if (int rc = exact_cg_run(a, w, 1, w.slot_of_round + round, picks + round, radius, cg_iters,
+                            cg_tol, s))
+    return rc;
   return exact_update_t<KIND>(a, qdiag, cache, sel, w, round, picks, s);
 }
 
 template <int KIND>
 int exact_refine_t(const EArgs& a, double* qdiag, double* cache, unsigned char* sel,
-                   const ExactWS& w, int slot, const long long* picks, int radius, int cg_iters,
-                   double cg_tol, hipStream_t s) {
+                   const ExactWS& w, int nb, const long long* cands, const int* slots,
+                   const long long* picks, int radius, int cg_iters, double cg_tol, hipStream_t s) {
   const long long nblk = ceil_div(a.n, EB);
-  double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
-  if (int rc = exact_cg_run(a, w, slot, w.cand, radius, cg_iters, cg_tol, x, s)) return rc;
+  if (int rc = exact_cg_run(a, w, nb, slots, cands, radius, cg_iters, cg_tol, s)) return rc;
   hipLaunchKernelGGL(exact_refine_end_kernel<KIND>, dim3(1), dim3(64), 0, s, a, qdiag, cache, sel, w,
-                     nblk, slot, picks);
+                     nblk, nb, slots, cands, picks);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -1224,17 +1385,33 @@ extern "C" int vgposp_exact_argmax(VGPOSP_EXACT_PARAMS, void* stream) {
   return 0;
 }
 
-extern "C" int vgposp_exact_refine(VGPOSP_EXACT_PARAMS, int slot, const int64_t* picks,
-                                   double cg_tol, void* stream) {
+extern "C" int vgposp_exact_refine(VGPOSP_EXACT_PARAMS, int nb, const int64_t* cands,
+                                   const int* slots, const int64_t* picks, double cg_tol,
+                                   void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_refine");
-  VG_CHECK_ARG(slot >= 0 && slot < exact_slots(kmax), 24);
-  VG_CHECK_ARG(picks != nullptr, 25);
-  VG_CHECK_ARG(cg_tol >= 0.0, 26);
+  VG_CHECK_ARG(nb >= 1 && nb <= CG_B, 24);
+  VG_CHECK_ARG(cands != nullptr, 25);
+  VG_CHECK_ARG(slots != nullptr, 26);
+  VG_CHECK_ARG(picks != nullptr, 27);
+  VG_CHECK_ARG(cg_tol >= 0.0, 28);
+  const long long* ck = reinterpret_cast<const long long*>(cands);
   const long long* pk = reinterpret_cast<const long long*>(picks);
   return dispatch_kind(kind, [&](auto K) {
     return exact_refine_t<decltype(K)::value>(a, const_cast<double*>(qdiag), cache, selected, w,
-                                              slot, pk, radius, cg_iters, cg_tol, s);
+                                              nb, ck, slots, pk, radius, cg_iters, cg_tol, s);
   });
+}
+
+extern "C" int vgposp_exact_topb(VGPOSP_EXACT_PARAMS, int B, int64_t* out, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_topb");
+  VG_CHECK_ARG(B >= 1 && B <= CG_B, 24);
+  VG_CHECK_ARG(out != nullptr, 25);
+  const long long nblk = ceil_div(a.n, EB), nsb = ceil_div(nblk, ESB);
+  ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
+  hipLaunchKernelGGL(exact_topb_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
+                     nblk, nsb, B, reinterpret_cast<long long*>(out));
+  VG_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int vgposp_exact_pick(VGPOSP_EXACT_PARAMS, int round, int slot, int64_t* picks,

@@ -395,7 +395,8 @@ def cg_iterations_for(lam_min, lam_max, tol=1e-16):
     return int(min(400, math.ceil(math.log(tol / 2) / math.log(rho)) + 4))
 
 
-BOUND_TMAX, BOUND_NBMAX = 14 * 64, 8192     # exact_bounds_kernel's register / LDS tables
+BOUND_TMAX, BOUND_NBMAX = 14 * 64, 8192
+REFINE_BATCH = 8        # candidates refined together by one batched CG (vgposp_exact_refine)     # exact_bounds_kernel's register / LDS tables
 BOUND_MARGIN = 1e-12                       # relative rounding margin on the upper bounds
 
 
@@ -447,7 +448,8 @@ class ExactWindowGreedy:
         self.ws = torch.empty(query("vgposp_exact_workspace_bytes", *prob.shape, prob.m, self.kmax,
                                     self.radius, self.cg_iters), dtype=torch.uint8, device=dev)
         self.nslots = 2 * self.kmax
-        self.refinements = 0
+        self.refinements = 0      # candidates refined (CG columns) in the last bounded run
+        self.refine_batches = 0   # batched CG solves in the last bounded run
         self.bound = None
 
     def _args(self, qdiag):
@@ -510,39 +512,63 @@ class ExactWindowGreedy:
              _p(self._tab[2]), self._T, K, scale, int(c0), c1, _stream())
         return b
 
-    def run_bounded(self, qdiag, k):
+    def run_bounded(self, qdiag, k, batch=None):
         """The rounds with qdiag holding upper bounds of Q_yy: the cache holds upper bounds of the
         reference's cached deltas; an arg-max that lands on a candidate whose Q_yy is only bounded
         refines it (its CG column; its cache entry becomes the reference's value) and the arg-max
-        is taken again, so every pick is the reference's arg-max.  One host read per arg-max."""
+        is taken again, so every pick is the reference's arg-max.  The refinement takes the
+        ``batch`` (<= 8) best entries together — one batched CG costs the launches of one column,
+        and the next rounds' picks are mostly among them.  One host read per top-B."""
         if k > self.kmax:
             raise ValueError(f"k = {k} > kmax = {self.kmax}")
+        B = REFINE_BATCH if batch is None else int(batch)
+        if not 1 <= B <= 8:
+            raise ValueError(f"batch must be in [1, 8], got {B}")
         self.picks.fill_(-1)
         args = self._args(qdiag)
         call("vgposp_exact_prepare", *args, 1, _stream())
-        cand_off = self._buffers()[4]
-        cand = self.ws[cand_off: cand_off + 8].view(torch.int64)
+        dev = self.p.device
+        top = torch.empty(9, dtype=torch.int64, device=dev)
+        cands = torch.empty(8, dtype=torch.int64, device=dev)
+        slots = torch.empty(8, dtype=torch.int32, device=dev)
         colslot, order, free = {}, [], list(range(self.nslots - 1, -1, -1))
-        self.refinements = 0
+        self.refinements = self.refine_batches = 0
         for t in range(k):
             while True:
-                call("vgposp_exact_argmax", *args, _stream())
-                c = int(cand.item())
+                call("vgposp_exact_topb", *args, B, _p(top), _stream())
+                got = top.cpu().tolist()
+                cnt = got[0]
+                c = got[1] if cnt > 0 else -1
                 if c < 0 or c in colslot:
                     break
-                if free:
-                    slot = free.pop()
-                else:  # recycle the oldest refined candidate that was not picked
-                    old = order.pop(0)
-                    slot = colslot.pop(old)
-                call("vgposp_exact_refine", *args, slot, _p(self.picks), self.cg_tol, _stream())
-                colslot[c] = slot
-                order.append(c)
-                self.refinements += 1
+                todo = [y for y in got[1:1 + cnt] if y not in colslot]
+                todo_set = set(todo)
+                use = []
+                for y in todo:
+                    if free:
+                        slot = free.pop()
+                    else:  # recycle the oldest refined candidate that is not picked or in the batch
+                        old = next((o for o in order if o not in todo_set), None)
+                        if old is None:
+                            break
+                        order.remove(old)
+                        slot = colslot.pop(old)
+                    use.append((y, slot))
+                cands[:len(use)].copy_(torch.tensor([y for y, _ in use], dtype=torch.int64))
+                slots[:len(use)].copy_(torch.tensor([s for _, s in use], dtype=torch.int32))
+                call("vgposp_exact_refine", *args, len(use), _p(cands), _p(slots), _p(self.picks),
+                     self.cg_tol, _stream())
+                for y, slot in use:
+                    colslot[y] = slot
+                    order.append(y)
+                self.refinements += len(use)
+                self.refine_batches += 1
             if c < 0:
                 break
             slot = colslot[c]
             order.remove(c)      # pinned: the pick's column is a row of Q_A
+            cand = self.ws[self._buffers()[4]:][:8].view(torch.int64)
+            cand.fill_(c)
             call("vgposp_exact_pick", *args, t, slot, _p(self.picks), _p(self.pick_delta),
                  _stream())
             if t < k - 1:
