@@ -518,7 +518,8 @@ class ExactWindowGreedy:
         refines it (its CG column; its cache entry becomes the reference's value) and the arg-max
         is taken again, so every pick is the reference's arg-max.  The refinement takes the
         ``batch`` (<= 8) best entries together — one batched CG costs the launches of one column,
-        and the next rounds' picks are mostly among them.  One host read per top-B."""
+        and the next rounds' picks are mostly among them.  One host read per arg-max (and one per
+        top-B when a refinement is due)."""
         if k > self.kmax:
             raise ValueError(f"k = {k} > kmax = {self.kmax}")
         B = REFINE_BATCH if batch is None else int(batch)
@@ -533,15 +534,17 @@ class ExactWindowGreedy:
         slots = torch.empty(8, dtype=torch.int32, device=dev)
         colslot, order, free = {}, [], list(range(self.nslots - 1, -1, -1))
         self.refinements = self.refine_batches = 0
+        cand = self.ws[self._buffers()[4]:][:8].view(torch.int64)
         for t in range(k):
             while True:
-                call("vgposp_exact_topb", *args, B, _p(top), _stream())
-                got = top.cpu().tolist()
-                cnt = got[0]
-                c = got[1] if cnt > 0 else -1
+                call("vgposp_exact_argmax", *args, _stream())
+                c = int(cand.item())
                 if c < 0 or c in colslot:
                     break
-                todo = [y for y in got[1:1 + cnt] if y not in colslot]
+                # the arg-max needs its column: refine the B best entries together
+                call("vgposp_exact_topb", *args, B, _p(top), _stream())
+                got = top.cpu().tolist()
+                todo = [y for y in got[1:1 + got[0]] if y not in colslot] or [c]
                 todo_set = set(todo)
                 use = []
                 for y in todo:
@@ -567,8 +570,6 @@ class ExactWindowGreedy:
                 break
             slot = colslot[c]
             order.remove(c)      # pinned: the pick's column is a row of Q_A
-            cand = self.ws[self._buffers()[4]:][:8].view(torch.int64)
-            cand.fill_(c)
             call("vgposp_exact_pick", *args, t, slot, _p(self.picks), _p(self.pick_delta),
                  _stream())
             if t < k - 1:
