@@ -926,14 +926,45 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_topb_kernel(const double* c
 
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
 
-// The cached delta of candidate y given the first nA picks (rows 0 .. nA-1 of LQ / LS, in global
-// memory), one wave: nominator s_yy - |LS^-1 s_Ay|^2, P = qyy - |LQ^-1 q_Ay|^2.  Lane s holds the
-// forward-substitution unknowns z_s and z_{s+64}; every lane returns the delta.
+// Rows of chol(Q_AA) / chol(S_AA + eps I): in the workspace (row stride kmax) or packed lower
+// triangles staged in LDS (row r at r (r + 1) / 2).
+struct FactorRows {
+  const double* lq;
+  const double* ls;
+  int stride;  // > 0: row stride; 0: packed
+  __device__ __forceinline__ int at(int r, int s) const {
+    return stride ? r * stride + s : r * (r + 1) / 2 + s;
+  }
+};
+
+__device__ __forceinline__ FactorRows global_rows(const ExactWS& w, int km) {
+  return FactorRows{w.LQ, w.LS, km};
+}
+
+// Stage rows 0 .. nr-1 of both factors as packed lower triangles into sm (2 nr (nr + 1) / 2
+// doubles), the whole workgroup.
+__device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int km, int nr, double* sm) {
+  const int np = nr * (nr + 1) / 2;
+  for (int e = threadIdx.x; e < 2 * np; e += blockDim.x) {
+    const int which = e >= np, k = which ? e - np : e;
+    int r = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
+    while (r * (r + 1) / 2 > k) --r;
+    while ((r + 1) * (r + 2) / 2 <= k) ++r;
+    const int s = k - r * (r + 1) / 2;
+    sm[e] = (which ? w.LS : w.LQ)[(size_t)r * km + s];
+  }
+  __syncthreads();
+  return FactorRows{sm, sm + np, 0};
+}
+
+// The cached delta of candidate y given the first nA picks, one wave: nominator
+// s_yy - |LS^-1 s_Ay|^2, P = qyy - |LQ^-1 q_Ay|^2.  Lane s holds the forward-substitution
+// unknowns z_s and z_{s+64}; every lane returns the delta.
 template <int KIND>
-__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const long long* picks, int nA,
-                               long long y, double qyy, bool exact) {
+__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRows& L,
+                               const long long* picks, int nA, long long y, double qyy,
+                               bool exact) {
   const int lane = threadIdx.x & 63;
-  const int km = a.kmax;
   double vs0 = 0.0, vq0 = 0.0, vs1 = 0.0, vq1 = 0.0;
   if (lane < nA) {
     vs0 = sigma_off<KIND>(a, picks[lane], y);
@@ -945,27 +976,26 @@ __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const long long
   }
   double zs0 = 0.0, zq0 = 0.0, zs1 = 0.0, zq1 = 0.0;
   for (int r = 0; r < nA; ++r) {
-    const double* ls = w.LS + (size_t)r * km;
-    const double* lq = w.LQ + (size_t)r * km;
     double ds = 0.0, dq = 0.0;
     if (lane < r) {
-      ds = ls[lane] * zs0;
-      dq = lq[lane] * zq0;
+      ds = L.ls[L.at(r, lane)] * zs0;
+      dq = L.lq[L.at(r, lane)] * zq0;
     }
     if (lane + 64 < r) {
-      ds = fma(ls[lane + 64], zs1, ds);
-      dq = fma(lq[lane + 64], zq1, dq);
+      ds = fma(L.ls[L.at(r, lane + 64)], zs1, ds);
+      dq = fma(L.lq[L.at(r, lane + 64)], zq1, dq);
     }
     ds = wave_sum(ds);
     dq = wave_sum(dq);
+    const double dls = L.ls[L.at(r, r)], dlq = L.lq[L.at(r, r)];
     if (r < 64) {
       if (lane == r) {
-        zs0 = (vs0 - ds) / ls[r];
-        zq0 = (vq0 - dq) / lq[r];
+        zs0 = (vs0 - ds) / dls;
+        zq0 = (vq0 - dq) / dlq;
       }
     } else if (lane == r - 64) {
-      zs1 = (vs1 - ds) / ls[r];
-      zq1 = (vq1 - dq) / lq[r];
+      zs1 = (vs1 - ds) / dls;
+      zq1 = (vq1 - dq) / dlq;
     }
   }
   const double ns = wave_sum(fma(zs0, zs0, zs1 * zs1));
@@ -988,7 +1018,8 @@ __global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* q
     const long long c = cands[j];
     if (c < 0) continue;
     const double qcc = qslot_at(w, slots[j], c, a.I1, a.I2);
-    const double d = wave_rescore<KIND>(a, w, picks, (int)w.lastA[c], c, qcc, true);
+    const double d = wave_rescore<KIND>(a, w, global_rows(w, a.kmax), picks, (int)w.lastA[c], c,
+                                        qcc, true);
     if (threadIdx.x == 0) {
       qdiag[c] = qcc;
       w.qexact[c] = 1;
@@ -1005,35 +1036,47 @@ __global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* q
 }
 
 // After q_t = Q e_{a_t}, part 1: row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I) (one wave
-// each).
+// each; the earlier rows staged in LDS when they fit, the right-hand sides computed by all lanes
+// at once, then one forward substitution with lane s holding z_s).
+constexpr int ROWS_LDS = 8192;  // doubles: packed rows of both factors up to |A| = 63
+
 template <int KIND>
 __global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int round,
                                                          const long long* picks) {
-  __shared__ double rowbuf[2][EX_KMAX];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ double sm[ROWS_LDS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int km = a.kmax;
   const long long at = picks[round];
   if (at < 0) return;
-  const double* L = wave == 0 ? w.LQ : w.LS;
-  double* row = rowbuf[wave];
-  for (int r = 0; r <= round; ++r) {
-    const long long ar = picks[r];
-    double v;
-    if (wave == 0) v = qcol_at(w, round, ar, a.I1, a.I2);
-    else v = (r == round) ? sigma_diag<KIND>(a) + a.jitter : sigma_off<KIND>(a, at, ar);
-    double acc = 0.0;
-    // off-diagonal: row . L[r][:r];  diagonal (r == round): |row[:r]|^2
-    for (int s = lane; s < r; s += 64)
-      acc = fma(row[s], r == round ? row[s] : L[(size_t)r * km + s], acc);
-    acc = wave_sum(acc);
-    v -= acc;
-    if (lane == 0) row[r] = (r == round) ? sqrt(v) : v / L[(size_t)r * km + r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, km, round, sm)
+                                                        : global_rows(w, km);
+  const double* Lm = wave == 0 ? L.lq : L.ls;
+  auto val = [&](int r) {
+    if (wave == 0) return qcol_at(w, round, picks[r], a.I1, a.I2);
+    return r == round ? sigma_diag<KIND>(a) + a.jitter : sigma_off<KIND>(a, at, picks[r]);
+  };
+  const double v0 = lane <= round ? val(lane) : 0.0;
+  const double v1 = lane + 64 <= round ? val(lane + 64) : 0.0;
+  double z0 = 0.0, z1 = 0.0;
+  for (int r = 0; r < round; ++r) {
+    double d = 0.0;
+    if (lane < r) d = Lm[L.at(r, lane)] * z0;
+    if (lane + 64 < r) d = fma(Lm[L.at(r, lane + 64)], z1, d);
+    d = wave_sum(d);
+    const double dl = Lm[L.at(r, r)];
+    if (r < 64) {
+      if (lane == r) z0 = (v0 - d) / dl;
+    } else if (lane == r - 64) {
+      z1 = (v1 - d) / dl;
+    }
   }
-  double* Lw = wave == 0 ? w.LQ : w.LS;
-  for (int s = lane; s <= round; s += 64) Lw[(size_t)round * km + s] = row[s];
+  const double nz = wave_sum(fma(z0, z0, z1 * z1));
+  double* Lw = (wave == 0 ? w.LQ : w.LS) + (size_t)round * km;
+  if (lane < round) Lw[lane] = z0;
+  if (lane + 64 < round) Lw[lane + 64] = z1;
+  // diagonal: sqrt(v_round - |z|^2), v_round held by lane round % 64
+  const double vr = __shfl(round < 64 ? v0 : v1, round & 63, 64);
+  if (lane == 0) Lw[round] = sqrt(vr - nz);
 }
 
 struct Window {
@@ -1059,9 +1102,14 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
                                                            double* cache, const unsigned char* sel,
                                                            ExactWS w, int round,
                                                            const long long* picks) {
+  __shared__ double sm[ROWS_LDS];
   const long long at = picks[round];
   if (at < 0) return;
   const Window v = window_of(a, at);
+  // every candidate of the workgroup walks the same factor rows: stage them once
+  const int nr = round + 1;
+  const FactorRows L = nr * (nr + 1) <= ROWS_LDS ? stage_rows(w, a.kmax, nr, sm)
+                                                 : global_rows(w, a.kmax);
   const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= v.w0 * v.w1 * v.w2) return;
   const long long y = ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) * a.I2 +
@@ -1070,7 +1118,7 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
     if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
     return;
   }
-  const double d = wave_rescore<KIND>(a, w, picks, round + 1, y, qdiag[y], w.qexact[y] != 0);
+  const double d = wave_rescore<KIND>(a, w, L, picks, round + 1, y, qdiag[y], w.qexact[y] != 0);
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
