@@ -109,6 +109,24 @@ def test_bounded_alg3_matches_oracle(shape, k, cutoff, beta, kind):
     assert g.refine_batches <= 2 * k and k <= g.refinements <= 8 * g.refine_batches
 
 
+@pytest.mark.parametrize("shape,k,cutoff", [
+    ((1, 1, 40), 6, 3),      # a line of candidates
+    ((2, 3, 50), 9, 2),
+    ((5, 6, 7), 1, 3),       # k = 1: round 0 only
+    ((6, 5, 4), 10, 0),      # cutoff 0: empty windows, the top-k of round 0
+    ((3, 3, 3), 27, 1),      # every candidate placed
+])
+def test_bounded_edge_cases_match_oracle(shape, k, cutoff):
+    from vgposp_amd.sparse_placement import tapered_placement_algorithm_3
+    X, ls = _grid(shape, seed=sum(shape) + k)
+    A, d, _ = tapered_placement_algorithm_3(X, k, shape, cutoff, 4.0, ls=ls, diag_shift=SHIFT,
+                                            method="bounds")
+    C = _dense(X, shape, 4.0, ls)
+    rA, _, rdci = op.placement_window_precision(C, k, shape, cutoff)
+    assert [int(a) for a in A] == rA
+    np.testing.assert_allclose(d, [rdci[a, i] for i, a in enumerate(rA)], rtol=1e-10, atol=1e-14)
+
+
 @pytest.mark.parametrize("shape,beta,kind", [
     ((12, 11, 10), 4.0, "eq"),
     ((9, 10, 11), 4.0, "matern52"),

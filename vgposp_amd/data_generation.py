@@ -105,8 +105,10 @@ def create_random_cov(n, rng=None):
 
 
 def grid_spacing(shape, extent=4.0):
-    """Uniform spacing h: the smallest axis spans ``extent`` (linspace(-2, 2, n) for a cube)."""
-    return extent / (min(shape) - 1)
+    """Uniform spacing h: the smallest axis with more than one point spans ``extent``
+    (linspace(-2, 2, n) for a cube); ``extent`` for a single point."""
+    n = min((int(s) for s in shape if int(s) > 1), default=2)
+    return extent / (n - 1)
 
 
 def grid_points(shape=(8, 8, 8), jitter=0.0, seed=0, extent=4.0):
