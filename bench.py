@@ -241,6 +241,7 @@ def vgp_line(args, which="c3", precision="fp64", world=1, rank=0, barrier=None, 
     if barrier:
         barrier()
     dt = (maxtime(time.perf_counter() - t0) if maxtime else time.perf_counter() - t0) / args.vgp_steps
+    train_op.check()  # the last step's Cholesky statuses (each earlier one: at the next run)
     # GEMM share from one more step run eagerly with the library's event timing on
     _lib.prof_enable(True)
     train_op.run({xb: Xd[idx[1]], yb: yd[idx[1]]})

@@ -241,9 +241,33 @@ def test_graph_30_replays_status(torch_dev, precision):
             Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
             out = [train_op.run({xb: Xd[i], yb: yd[i]}) for i in idx]
             losses[mode] = [float(v) for v in out]
+            train_op.check()  # the last replayed step's statuses (the others: at each next run)
             if mode == "1":
                 assert train_op._g is not None
                 assert int(torch.count_nonzero(train_op._g[5])) == 0
         finally:
             os.environ.pop("VGPOSP_GRAPH", None)
     assert losses["1"] == losses["0"]
+
+
+def test_graph_replay_failed_factorization_raises_one_run_late(torch_dev):
+    """A replayed step whose Cholesky fails (NaN inducing points) raises CholeskyError from the
+    next run() (or check()): the statuses are read behind the next step, not by draining the
+    queue after every replay."""
+    from vgposp_amd._lib import CholeskyError
+    from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
+    torch = torch_dev
+    X, y, Z = vgp_c3_data(n=32, m=6, half=7.0)
+    N = len(X)
+    B = N // 8
+    train_op, _, xb, yb = vgp_c3_graph(X, y, Z, B)
+    Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
+    idx = torch.arange(B, device="cuda")
+    for _ in range(3):
+        train_op.run({xb: Xd[idx], yb: yd[idx]})
+    assert train_op.graph and train_op._g is not None
+    train_op.check()
+    train_op.theta[train_op.z_off] = float("nan")
+    train_op.run({xb: Xd[idx], yb: yd[idx]})          # issued; its status not read yet
+    with pytest.raises(CholeskyError):
+        train_op.run({xb: Xd[idx], yb: yd[idx]})      # reads the failed step's status

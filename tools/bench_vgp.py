@@ -64,6 +64,7 @@ def main():
         l_ = train_op.run({xb: Xd[batches[i]], yb: yd[batches[i]]})
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    train_op.check()
     losses.append(float(l_))
     # per-kernel breakdown from eager steps with the library's event timing on (no graph)
     _lib.prof_enable(True)

@@ -125,7 +125,9 @@ class VGPTrainOp:
 
     From the second run on, the whole step (posterior, ELBO, reverse pass, Adam: ~400 launches)
     is captured once into a HIP graph and replayed, with the feeds copied into static buffers —
-    the same fixed graph a TF1 session runs.  Eager when ``graph=False``, ``VGPOSP_GRAPH=0``, for
+    the same fixed graph a TF1 session runs.  A replayed step's Cholesky statuses are checked
+    when the next step has been issued (or by ``check()``), so a non-PD factorization raises
+    CholeskyError one ``run`` late.  Eager when ``graph=False``, ``VGPOSP_GRAPH=0``, for
     a data-parallel ``group``, or while the library's event timing is on."""
 
     def __init__(self, loss, opt, var_list=None, group=None, graph=True, precision="fp64"):
@@ -179,6 +181,8 @@ class VGPTrainOp:
         self.graph = bool(graph) and group is None and os.environ.get("VGPOSP_GRAPH", "1") != "0"
         self._runs = 0
         self._g = None  # (graph, feed shapes, static X, static y, loss, statuses)
+        self._hstat = None    # two pinned host buffers for the replayed steps' statuses
+        self._pending = None  # (event, buffer) of the last replayed step, not yet checked
 
     def _value(self, p):
         return resolve(p).reshape(())
@@ -211,12 +215,38 @@ class VGPTrainOp:
         sX.copy_(Xb)
         sy.copy_(yb)
         g.replay()
-        # stream-ordered status read (one host sync per step, inside check_info).  The captured
-        # step holds only kernel nodes: the library's fills / 2-D copies are kernels
-        # (common.h vg_memset / vg_memcpy2d), which removed the stale-status reads seen when
-        # memset / memcpy nodes were replayed back to back (commit 4d967c4's host sync).
-        linalg.check_info(status)
-        return loss.clone()
+        out = loss.clone()
+        # The step's Cholesky statuses go to pinned host memory behind the replay and are checked
+        # when the NEXT step has been issued (or by check()): waiting then costs nothing, the GPU
+        # already holds that step, so the host never drains the queue between steps.  The
+        # captured step holds only kernel nodes (the library's fills / 2-D copies are kernels,
+        # common.h vg_memset / vg_memcpy2d), which removed the stale-status reads round 2 saw
+        # when memset / memcpy nodes were replayed back to back.
+        if self._hstat is None or self._hstat[0].numel() != status.numel():
+            self._hstat = [torch.empty(status.numel(), dtype=status.dtype, pin_memory=True)
+                           for _ in range(2)]
+        buf = self._hstat[self._runs & 1]
+        prev = self._pending
+        if prev is not None and prev[1] is buf:
+            self.check()
+            prev = None
+        buf.copy_(status, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending = (ev, buf)
+        if prev is not None:
+            prev[0].synchronize()
+            linalg.check_info(prev[1])
+        return out
+
+    def check(self):
+        """Check the statuses of the last replayed step (its factorizations were PD); ``run``
+        checks each step's when the next one has been issued."""
+        if self._pending is not None:
+            ev, buf = self._pending
+            self._pending = None
+            ev.synchronize()
+            linalg.check_info(buf)
 
     def run(self, feed=None):
         yb, Xb = self.loss.inputs(feed)
@@ -228,6 +258,7 @@ class VGPTrainOp:
         if self.graph and self._runs > 0 and not _lib.prof_on():
             loss = self._replay(Xb, yb)
         else:
+            self.check()
             loss = self._step(Xb, yb)
         self._runs += 1
         self.loss.value = loss
