@@ -1,5 +1,6 @@
-"""Config C4 on the GPU: the local-kernel greedy (vgposp_local_*) against the oracle's restatement
-of snippets_a3.sparse_placement_algorithm_3 with local deltas — picks bit-exact, the
+"""The epsilon-local APPROXIMATION of config C4 (vgposp_local_*; the exact C4 path is
+sparse_placement, tests/test_gpu_exact.py) against the oracle's restatement of the same
+approximation (snippets_a3.sparse_placement_algorithm_3 with local deltas) — picks bit-exact, the
 delta_cached_iters snapshots to rounding — over every lane-group width (taper supports of 7, 27,
 33 and 57 points), four kernels, window cutoffs 0-3, ragged grids, a 2-rank candidate-sharded run
 on one GPU, and the full 128^3 k = 50 sequence."""

@@ -568,7 +568,7 @@ __device__ __forceinline__ void wave_refresh_keys(const double* cache, const uns
 // (snippets_a3.py:162-168), its keys refreshed; CG set up for q = Q e_{y*} in slot `round`.
 __global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
     double* cache, unsigned char* sel, long long I0, long long I1, long long I2, ExactWS w,
-    long long nblk, long long nsb, int round, long long* picks, double* pick_delta, int solve) {
+    long long nblk, long long nsb, int round, long long* picks, double* pick_delta) {
   const long long n = I0 * I1 * I2;
   const long long a = block_argmax(w, nsb);
   if (threadIdx.x == 0) {
@@ -1296,7 +1296,7 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
   {
     ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
     hipLaunchKernelGGL(exact_select_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, sel, a.I0, a.I1,
-                       a.I2, w, nblk, nsb, round, picks, pick_delta, last ? 0 : 1);
+                       a.I2, w, nblk, nsb, round, picks, pick_delta);
     VG_LAUNCH_CHECK();
   }
   if (last) return 0;
