@@ -77,6 +77,9 @@ struct ExactWS {
   size_t bytes;
 };
 
+// coefficient rows padded to an even count of doubles (16-byte aligned rows: two-double loads)
+__host__ __device__ constexpr int coef_stride(int m) { return (m + 1) & ~1; }
+
 // column slots: one per pick, as many again for refined candidates that are not (yet) picked
 __host__ __device__ __forceinline__ int exact_slots(int kmax) { return 2 * kmax; }
 
@@ -102,7 +105,7 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
     off += ealign(b);
     return r;
   };
-  w.coef = (double*)take(8 * (size_t)n * m);
+  w.coef = (double*)take(8 * (size_t)n * coef_stride(m));
   w.bval = (double*)take(8 * nblk);
   w.bidx = (long long*)take(8 * nblk);
   w.sval = (double*)take(8 * nsb);
@@ -197,8 +200,9 @@ __global__ __launch_bounds__(256) void exact_coef_kernel(EArgs a, double* __rest
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   const int m = a.m1 + 1;
-  double* c = coef + i * m;
+  double* c = coef + i * coef_stride(m);
   c[0] = sigma_diag<KIND>(a) + a.jitter;
+  if (coef_stride(m) > m) c[m] = 0.0;
   const long long i0 = i / (a.I1 * a.I2), i1 = (i / a.I2) % a.I1, i2 = i % a.I2;
   for (int o = 0; o < a.m1; ++o) {
     const int o0 = a.offs[3 * o], o1 = a.offs[3 * o + 1], o2 = a.offs[3 * o + 2];
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(256) void exact_gersh_kernel(const double* __restri
   double lo = INFINITY, hi = -INFINITY;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
-    const double* c = coef + i * m;
+    const double* c = coef + i * coef_stride(m);
     double s = 0.0;
     for (int o = 1; o < m; ++o) s += fabs(c[o]);
     lo = fmin(lo, c[0] - s);
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
         const int j = s * 64 + lane;
         q[s] = 0.0;
         if (s * 64 < cnt && j < cnt && gi[s] >= 0) {
-          const double* c = coef + (size_t)gi[s] * m;
+          const double* c = coef + (size_t)gi[s] * coef_stride(m);
           double acc = c[0] * p[s];
           const short* nb = nbl + j * m1;
           for (int o = 0; o < m1; ++o) {
@@ -396,8 +400,15 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
         if (g0 >= 0 && g0 < I0 && g1 >= 0 && g1 < I1 && g2 >= 0 && g2 < I2)
           gi = (g0 * I1 + g1) * I2 + g2;
       }
+      // the padded row in two-double loads
+      constexpr int MS = coef_stride(M);
 #pragma unroll
-      for (int o = 0; o < M; ++o) c[s][o] = gi >= 0 ? coef[gi * M + o] : 0.0;
+      for (int o = 0; o < MS; o += 2) {
+        double2 v = make_double2(0.0, 0.0);
+        if (gi >= 0) v = *reinterpret_cast<const double2*>(coef + gi * MS + o);
+        if (o < M) c[s][o] = v.x;
+        if (o + 1 < M) c[s][o + 1] = v.y;
+      }
       r[s] = (j == 0) ? 1.0 : 0.0;
       p[s] = r[s];
       pl[j] = r[s];
@@ -757,7 +768,7 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
                     g2 = q.c2 + t % q.e2;
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     const double pi = it == 0 ? cc.r[l] : fma(beta, pold[l], cc.r[l]);
-    const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * m;
+    const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * coef_stride(m);
     double s = c[0] * pi;
     for (int o = 0; o < m1; ++o) {
       const double cv = c[1 + o];
