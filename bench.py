@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--vgp-steps", type=int, default=10)
     p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 exact algorithm 3) line")
     p.add_argument("--c4-steps", type=int, default=10)
+    p.add_argument("--no-sweep", action="store_true",
+                   help="skip the 32^3 / 64^3 / 128^3 grid sweep")
     p.add_argument("--no-c4-selinv", action="store_true",
                    help="skip the C4 selected-inverse cross-check run")
     p.add_argument("--no-splits", action="store_true",
@@ -440,6 +442,95 @@ def c4_line(args, world, rank, barrier, maxtime):
     return out
 
 
+def grid_sweep(args, world, rank, barrier, maxtime):
+    """north_star's grid sizes: placements/s of k = 50 on 32^3, 64^3 and 128^3 at
+    this run's GPU count.  32^3 (N = 32,768): the dense exact lazy greedy of the headline
+    (placement_algorithm_2; sharded at N > 1) with its GEMM's fraction of the fp64 MFMA peak;
+    64^3 and 128^3: the exact algorithm 3 on the beta = 4 tapered covariance (config C4's form: no
+    dense cov_vv fits, 64^3 dense would be 550 GB), latency-bound, so no roofline fraction."""
+    import torch
+
+    from vgposp_amd import _lib, linalg
+    from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    from vgposp_amd.sharded_placement import HipGreedyBackend, ShardedGreedyPlacement
+    from vgposp_amd.sparse_placement import ExactTaperPlacement
+    from vgposp_amd.workloads import c4_grid, placement_split
+    k = 50
+    out = {}
+    # 32^3 dense
+    shape = (32, 32, 32)
+    X, ls = placement_split(shape, 0)
+    N = len(X)
+    Xd = linalg.as_device(X)
+    amp_d, ls_d, sh_d = (linalg.as_device([v]) for v in (1.0, ls, args.noise + 1e-6))
+    S = torch.empty((N, N), dtype=torch.float64, device="cuda")
+    if world == 1:
+        g = GreedyPlacement(S, k)
+
+        def rounds():
+            g.init()
+            for _ in range(k):
+                g.step(lazy=True)
+    else:
+        sh = ShardedGreedyPlacement(HipGreedyBackend(S, k), partition_inverse=True)
+        g = sh.b.g
+
+        def rounds():
+            sh.run(k)
+
+    def step():
+        linalg.kernel_matrix("eq", Xd, None, amp_d, ls_d, diag_shift=sh_d, out=S[None])
+        rounds()
+
+    step()
+    torch.cuda.synchronize()
+    g.check()
+    reps = 3
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = maxtime(time.perf_counter() - t0) / reps
+    g.check()
+    _lib.prof_enable(True)
+    step()
+    torch.cuda.synchronize()
+    gms, _, gfl, _ = _lib.prof_query("gemm_f64")
+    _lib.prof_enable(False)
+    gtf = gfl / (gms * 1e-3) / 1e12 if gms else None
+    out["32^3_dense_alg2"] = {"N": N, "placements_per_s": k / dt, "ms_per_problem": dt * 1e3,
+                              "gemm_tflops": gtf,
+                              "gemm_frac_of_fp64_mfma": gtf / FP64_MFMA_PEAK_TFLOPS if gtf else None,
+                              "selected_head": [int(v) for v in g.selected[:6].cpu()]}
+    del S, g
+    torch.cuda.empty_cache()
+    # 64^3 and 128^3 tapered exact algorithm 3
+    for n in (64, 128):
+        Xc, shp, lsc = c4_grid(n)
+        run = ExactTaperPlacement(Xc, shp, k, 3, 4.0, ls=lsc, diag_shift=args.noise + 1e-6,
+                                  method="bounds")
+        run.run()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            run.run()
+        torch.cuda.synchronize()
+        barrier()
+        dt = maxtime(time.perf_counter() - t0) / 5
+        out[f"{n}^3_tapered_alg3"] = {"N": n ** 3, "placements_per_s": k / dt,
+                                      "ms_per_problem": dt * 1e3,
+                                      "picks_head": [int(v) for v in run.greedy.picks[:6].cpu()]}
+        del run
+        torch.cuda.empty_cache()
+    out["note"] = ("k = 50 each; 32^3: jittered grid, EQ ls 2h, noise 1e-2 + 1e-6 (the headline's "
+                   "workload at N = 32,768); 64^3 / 128^3: config C4's taper (beta 4, cutoff 3)")
+    return out
+
+
 def splits_line(args, world, barrier, maxtime, rank):
     """N > 1 extra: one independent 64x32x32 split per rank (weak scaling, no collective)."""
     import torch
@@ -603,6 +694,7 @@ def main():
     torch.cuda.empty_cache()
 
     c4 = None if args.no_c4 else c4_line(args, world, rank, barrier, maxtime)
+    sweep = None if args.no_sweep else grid_sweep(args, world, rank, barrier, maxtime)
     vgp = None
     if not args.no_vgp:
         kw = dict(world=world, rank=rank, barrier=barrier, maxtime=maxtime)
@@ -705,6 +797,8 @@ def main():
     }
     if c4 is not None:
         out["c4"] = c4
+    if sweep is not None:
+        out["grid_sweep"] = sweep
     if splits is not None:
         out["independent_splits"] = splits
     if vgp is not None:
