@@ -439,6 +439,20 @@ def c4_line(args, world, rank, barrier, maxtime):
                     "fp64 MFMA fronts, then the plain rounds; one profiled run"}
         del sel
         torch.cuda.empty_cache()
+    # the CPU side: the plain-C restatement (oracle/c4_exact.c, OpenMP) on the whole workload —
+    # its picks are the "bit-exact vs CPU" check at full size, its time the C4 CPU baseline
+    if world == 1 and rank == 0 and not args.no_cpu:
+        from oracle import c4_exact as oc4
+        st = {}
+        cp, _ = oc4.exact_alg3(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6,
+                               stats=st)
+        out["cpu_baseline"] = {
+            "value": k / st["seconds"], "unit": "placements/s", "cores": st["threads"],
+            "kind": "port", "sample": f"the whole workload (128^3, k={k}), one run",
+            "picks_equal": [int(v) for v in cp] == picks, "seconds": st["seconds"],
+            "refinements": st["refinements"],
+            "note": "oracle/c4_exact.c: the same bounded-lazy algorithm 3 in C (OpenMP bounds, "
+                    "sequential rounds)"}
     return out
 
 

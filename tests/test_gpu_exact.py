@@ -5,6 +5,7 @@ without a dense cov_vv, checked against the reference semantics.
 * the CG columns Q e_a against the dense inverse's columns;
 * picks, pick deltas and delta_cached_iters against the oracle's restatement of
   snippets_a3.sparse_placement_algorithm_3 on the dense tapered matrix (small grids);
+* picks against the plain-C restatement (oracle/c4_exact.c) at 48x40x56 .. 128^3;
 * picks against the dense algorithm-3 engine on the GPU (snippets_a3.placement_algorithm_3 over
   the dense tapered covariance) on every grid where that matrix fits: 16^3, 24^3, 32^3, 40^3."""
 import numpy as np
@@ -275,3 +276,23 @@ def test_exact_128cube_regression(method):
     A, _, _ = tapered_placement_algorithm_3(X, 50, shape, 3, 4.0, ls=ls, diag_shift=SHIFT,
                                             method=method)
     assert [int(a) for a in A] == want
+
+
+@pytest.mark.parametrize("shape,k,cutoff,kind,seed", [
+    ((128, 128, 128), 50, 3, "eq", 1),
+    ((64, 64, 64), 50, 2, "matern52", 3),
+    ((48, 40, 56), 60, 4, "matern32", 5),
+    ((96, 80, 72), 40, 3, "eq", 7),
+])
+def test_bounded_alg3_matches_c_oracle_at_scale(shape, k, cutoff, kind, seed):
+    """GPU picks bit-exact against the CPU: the bounded-lazy algorithm 3 on the device and the
+    plain-C restatement (oracle/c4_exact.c, tests/test_c4_oracle.py pins it to the dense oracle) on
+    the host, at north_star's sizes (no dense matrix fits), with pick deltas within 1e-10."""
+    from oracle import c4_exact as ce
+    from vgposp_amd.sparse_placement import tapered_placement_algorithm_3
+    X, ls = _grid(shape, seed=seed)
+    A, d, _ = tapered_placement_algorithm_3(X, k, shape, cutoff, 4.0, kernel=kind, ls=ls,
+                                            diag_shift=SHIFT, method="bounds")
+    cp, cd = ce.exact_alg3(X, shape, k, cutoff, 4.0, kind=kind, ls=ls, diag_shift=SHIFT)
+    assert [int(a) for a in A] == [int(a) for a in cp]
+    np.testing.assert_allclose(d, cd, rtol=1e-10)
