@@ -256,7 +256,13 @@ __global__ __launch_bounds__(256) void gemm_ref_kernel(GemmParams p, int vec_a, 
 #ifndef VGPOSP_GEMM_OCC
 #define VGPOSP_GEMM_OCC 2
 #endif
+#ifndef VGPOSP_GEMM_SPREAD2
+#define VGPOSP_GEMM_SPREAD2 2
+#endif
 constexpr int STAGES = VGPOSP_GEMM_STAGES;
+// 2-stage ring: 0 = the next K-tile's pieces issued right after the barrier, S > 0 = spread over
+// the first S k-slices, after each slice's fragment reads
+constexpr int SPREAD2 = VGPOSP_GEMM_SPREAD2;
 constexpr int OPND_ELEMS = GBM * GBK;        // 2048 doubles = 16 KiB per operand per stage
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -321,7 +327,7 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   constexpr int SE = (NSUB + 1) * OPND_ELEMS;          // doubles per stage: A subs | B
   constexpr int PO = 16 / NW;                          // pieces per operand per wave
   constexpr int PPW = PO * (NSUB + 1);                 // pieces per wave per stage (8, 12 or 6)
-  constexpr bool SPREAD = NST >= 3;                    // next-tile loads between the MFMAs
+  constexpr bool SPREAD = NST >= 3 || SPREAD2 > 0;     // next-tile loads between the MFMAs
   constexpr bool A_IL = false, B_IL = false;  // plain fragment order
   __shared__ __attribute__((aligned(16))) double smem[NST * SE];
 
@@ -429,7 +435,9 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     __builtin_amdgcn_s_barrier();
     // 3-stage ring: the next K-tile's pieces are spread over the k-slices below, between MFMAs
     // (issued back to back they park the wave for their issue cost; 8192^3 NT 63.3 -> 65.7 TF/s).
-    // 2-stage ring: issued here, as early as possible — the tile is needed one K-step later.
+    // 2-stage ring: spread over the first SPREAD2 k-slices, each after that slice's fragment reads
+    // (the reads no longer wait behind the piece issue after the barrier; 65k step 16.10 ->
+    // 16.23 placements/s over three interleaved repeats); SPREAD2 = 0 issues them all here.
     const bool more = t + NST - 1 < T;
     if (!SPREAD && more) issue(t + NST - 1);
 
@@ -468,8 +476,11 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
         }
       }
       if (SPREAD && more) {
+        constexpr int NS = NST >= 3 ? 4 : (SPREAD2 > 0 ? SPREAD2 : 4);
+        if (ks < NS) {
 #pragma unroll
-        for (int q = (ks * PPW) / 4; q < ((ks + 1) * PPW) / 4; ++q) issue_piece(t + NST - 1, q);
+          for (int q = (ks * PPW) / NS; q < ((ks + 1) * PPW) / NS; ++q) issue_piece(t + NST - 1, q);
+        }
       }
 #pragma unroll
       for (int i = 0; i < FI; ++i)
