@@ -150,9 +150,22 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   if (linv) linv += (int64_t)blockIdx.x * stride_linv;
   if (diag_out) diag_out += (int64_t)blockIdx.x * (stride_diag < 0 ? jb : stride_diag);
   const int JP = (jb + LW - 1) & ~(LW - 1), NP = JP / LW;
-  for (int e = t; e < NB * NB; e += LEAF_THREADS) {
-    const int r = e / NB, c = e % NB;
-    if (r < JP && c <= r) L[r * LP2 + c] = r < jb ? A[(int64_t)r * lda + c] : (r == c ? 1.0 : 0.0);
+  // Block load: thread t reads column t & 127 of rows 2u + (t >> 7), 16 loads in flight per
+  // batch from clamped (always valid) addresses; a loop with one load per iteration waited on each
+  // load in turn (64 round trips, about half of the leaf's time).
+  for (int u0 = 0; u0 < NB / 2; u0 += 16) {
+    double v[16];
+    const int c = t & (NB - 1), cc = min(c, jb - 1);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = 2 * (u0 + u) + (t >> 7);
+      v[u] = A[(int64_t)min(r, jb - 1) * lda + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = 2 * (u0 + u) + (t >> 7);
+      if (r < JP && c <= r) L[r * LP2 + c] = (r < jb && c < jb) ? v[u] : (r == c ? 1.0 : 0.0);
+    }
   }
   if (!factor)
     for (int c = t; c < JP; c += LEAF_THREADS) rdiag[c] = c < jb ? 1.0 / A[(int64_t)c * lda + c] : 1.0;
