@@ -15,4 +15,4 @@ run() {  # name, bench_vgp args
 }
 run c3
 run c5 --c5 --kernel matern52
-run c5m --c5 --kernel matern52 --mixed --mixed-iters 2
+# run c5m --c5 --kernel matern52 --mixed --mixed-iters 2
