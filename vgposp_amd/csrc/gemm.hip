@@ -939,10 +939,15 @@ static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa =
   // 10 lower tiles x 52 splits = 520 > 512 ran as slowly as the 16-tile full product)
   int64_t s = 512 / nblk;
   // long K: splits at least 512 deep.  Short K (few output tiles, e.g. the M x M products of the
-  // VGP step, 16 tiles of a 512^3 product on 16 CUs): up to 8 splits, at least 64 deep — each
-  // split's 128x128 partial costs 256 KB of HBM traffic, about the time of 64 K-steps on one CU.
+  // VGP step, 16 tiles of a 512^3 product on 16 CUs, and the Cholesky recursion's 128..1024
+  // levels): up to 8 splits, at least 16 deep (one K-tile).  Measured against 64 deep (the
+  // VGPOSP_SPLIT_MIN_K override, profiles/r3_vgp_ab_streams_splitk_*.jsonl): C3 6.30 -> 6.19 ms,
+  // C5 7.32 -> 7.26 ms, the 65k step unchanged (16.27 vs 16.30 placements/s): a split's partial
+  // costs less than the serial K-steps it removes from a latency-bound chain.
   const int64_t deep = k / 512;
-  s = std::min<int64_t>(s, deep >= 8 ? deep : std::min<int64_t>(8, k / 64));
+  const char* env = std::getenv("VGPOSP_SPLIT_MIN_K");
+  const int64_t min_k = env ? std::max<int64_t>(16, std::atoll(env)) : (int64_t)16;
+  s = std::min<int64_t>(s, deep >= 8 ? deep : std::min<int64_t>(8, k / min_k));
   return (int)std::max<int64_t>(s, 1);
 }
 

@@ -29,6 +29,7 @@ replicated and never reduced.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -111,6 +112,12 @@ def _col(v):
     return v.reshape(-1, 1)
 
 
+def _wait(a, b):
+    """Stream a waits for the work enqueued so far on stream b (nothing when they are one)."""
+    if a is not b:
+        a.wait_stream(b)
+
+
 class VGPObjective:
     """Negative ELBO of the reference's VGP training graph and its gradient, for one kernel.
 
@@ -143,6 +150,8 @@ class VGPObjective:
         self.group = group
         self._Kzx = None
         self._side = None
+        self._tail = None  # side streams of the step (Kzb, the vector chain, VJPs, reductions)
+        self._mat = None   # side stream of the M x M chain
 
     def _allreduce(self, t):
         """Sum over the data-parallel group (host-staged for gloo, in place on device for RCCL)."""
@@ -271,31 +280,75 @@ class VGPObjective:
         M, nb = Z.shape[0], yb.numel()
         check = infos is None
         infos = [] if check else infos  # Cholesky statuses, checked once at the end
+        # the minibatch's Kzb depends only on the inputs: with side streams on (bit 1) it is
+        # assembled beside the forward posterior's Kzx assembly and SYRK
+        main = torch.cuda.current_stream()
+        if self._tail is None:
+            # Side streams, bit 1: Kzb beside the forward pass, 2: the three middle chains, 4:
+            # VJPs and reductions beside G Kzx.  Measured per segment (tools/vgp_ab.py,
+            # profiles/r3_vgp_ab_streams_segments_*.jsonl): the fp64 step is fastest on ONE stream
+            # (C3 6.14 ms with none, 6.19-6.28 with any; C5 7.25 against 7.40-7.54), the mixed one
+            # with all three (9.15 against 9.72 ms: its factorizations already run on side streams).
+            self._streams = int(os.environ.get("VGPOSP_VGP_STREAMS", "7" if self.mixed else "0"))
+            self._tail, self._mat = torch.cuda.Stream(), torch.cuda.Stream()
+        use = self._streams
+        tail = self._tail if use & 1 else main
+        _wait(tail, main)
+        with torch.cuda.stream(tail):
+            Kzb = linalg.kernel_matrix(self.kind, Z, Xb, a, l)[0]
+        Kzb.record_stream(main)
         st = self._forward_posterior(Z, a, l, s, infos, side=True)
         Kzz, Kzx, P0, c, Li, t, m, A = (st[k] for k in
                                         ("Kzz", "Kzx", "P0", "c", "Li", "t", "m", "A"))
-        Kzb = linalg.kernel_matrix(self.kind, Z, Xb, a, l)[0]
+        _wait(main, tail)
         Kzj_inv, Lpi, Kp_inv, Kzz_inv = (st[k] for k in ("Kzj_inv", "Lpi", "Kp_inv", "Kzz_inv"))
         dev = Z.device
         # ---- variational loss (every scalar is taken at the end by vgposp_dots / _scalars) ----
-        v = linalg.gemm(Kzj_inv, _col(m))
-        r = yb.clone()
-        linalg.gemm(Kzb, v, _col(r), alpha=-1.0, beta=1.0, transa=True)  # r = yb - Kzb^T v
-        v = v.reshape(-1)
-        # Trace term with two M x B products instead of three: with H = Kzj^-1 Kzb (Kzj^-1 =
-        # Lzi^T Lzi) and R = op(A) H,  tr(G^T G) = <Kzb, H> for G = Lzi Kzb, and
-        # tr(R^T R) = <Q, H H^T> with Q = A^T A (A A^T for the trace_adjoint form).
-        H = linalg.gemm(Kzj_inv, Kzb)
-        HHt = linalg.gemm(H, H, transb=True, lower_c=True)
+        # Three independent chains until A_b: the SYRK Kzb Kzb^T and H H^T, the vector chain (v, r,
+        # u, m_b, c_b: GEMVs) and the M x M products of A; with side streams on (bit 2) the last two
+        # run on their own streams beside the first.  Every operand comes from before the fork;
+        # every result is read only after a join.
+        tail = self._tail if use & 2 else main
+        mat = self._mat if use & 2 else main
+        _wait(tail, main)
+        _wait(mat, main)
+        with torch.cuda.stream(tail):
+            v = linalg.gemm(Kzj_inv, _col(m))
+            r = yb.clone()
+            linalg.gemm(Kzb, v, _col(r), alpha=-1.0, beta=1.0, transa=True)  # r = yb - Kzb^T v
+            v = v.reshape(-1)
+            qm = linalg.gemm(Lpi, _col(m), tri_a=True)
+            if want_grads:
+                mu_b = _lincomb([(r, 1.0, -1)], s, shift=j)  # r / (s + j)
+                u = linalg.gemm(Kzj_inv, linalg.gemm(Kzb, _col(mu_b))).reshape(-1)
+                qv = linalg.gemm(Kp_inv, _col(m)).reshape(-1)
+                m_b = _lincomb([(u, 1.0, 0), (qv, -w, 0)])
+                t_b = linalg.gemm(Kzz, _col(m_b)) / s
+                c_b = linalg.gemm(Li, linalg.gemm(Li, t_b, tri_a=True), transa=True,
+                                  tri_a=True).reshape(-1)
+        with torch.cuda.stream(mat):
+            Q = linalg.gemm(A, A, transa=not self.trace_adjoint, transb=self.trace_adjoint)
+            PA = linalg.gemm(Lpi, A, tri_a=True)
+            if want_grads:
+                QA = linalg.gemm(Kp_inv, A)
+                P = linalg.gemm(Kzj_inv, Q)
+                W = _lincomb([(P, -1.0, -1)], s, diag=(1.0, -1))  # (I - P) / s
+                QAQA = linalg.gemm(QA, QA, transb=True)
+        # Trace terms from ONE M x B product, the SYRK Sb = Kzb Kzb^T: with H = Kzj^-1 Kzb
+        # (Kzj^-1 = Lzi^T Lzi) and R = op(A) H,  tr(G^T G) = <Kzb, H> = <Sb, Kzj^-1> for
+        # G = Lzi Kzb, and tr(R^T R) = <Q, H H^T> with Q = A^T A (A A^T for the trace_adjoint
+        # form) and H H^T = Kzj^-1 Sb Kzj^-1 (M x M products); H itself is never formed.
+        Sb = linalg.gemm(Kzb, Kzb, transb=True, lower_c=True)
+        call("vgposp_sym_from_lower", _p(Sb), M, M, _stream())
+        HHt = linalg.gemm(linalg.gemm(Kzj_inv, Sb), Kzj_inv, lower_c=True)
         call("vgposp_sym_from_lower", _p(HHt), M, M, _stream())
-        Q = linalg.gemm(A, A, transa=not self.trace_adjoint, transb=self.trace_adjoint)
-        PA = linalg.gemm(Lpi, A, tri_a=True)
-        qm = linalg.gemm(Lpi, _col(m), tri_a=True)
         sums = torch.zeros(13, dtype=F64, device=dev)  # VGPOSP_S_* of vgposp.h
-        fwd = [(r, 1, r, 1, nb, 0), (Kzb, 1, H, 1, M * nb, 0), (Q, 1, HHt, 1, M * M, 0),
+        fwd = [(r, 1, r, 1, nb, 0), (Sb, 1, Kzj_inv, 1, M * M, 0), (Q, 1, HHt, 1, M * M, 0),
                (PA, 1, PA, 1, M * M, 0), (qm, 1, qm, 1, M, 0), (st["lds"], 1, None, 0, M, 1),
                (st["ldp"], 1, None, 0, M, 1), (st["ldk"], 1, None, 0, M, 1)]
         if not want_grads:
+            _wait(main, tail)
+            _wait(main, mat)
             _dots(fwd, sums)
             zero = torch.zeros(2, dtype=F64, device=dev)
             out = torch.empty(4, dtype=F64, device=dev)
@@ -306,35 +359,38 @@ class VGPObjective:
                     linalg.check_info(info)
             return out[0], None, None, None, None
         # ---- reverse pass (d E) ----
-        mu_b = _lincomb([(r, 1.0, -1)], s, shift=j)  # r / (s + j)
-        u = linalg.gemm(Kzj_inv, linalg.gemm(Kzb, _col(mu_b))).reshape(-1)
         # dE/dR = -R / s gives A_b = -(1/s) A HHt (HHt A for trace_adjoint) and H_b = -(1/s) Q H;
         # through H = Kzj^-1 Kzb: Kzb_b += Kzj^-1 H_b, Kzz_b -= Kzj^-1 H_b H^T.  With
         # P = Kzj^-1 Q all of it is M x M work plus one M x B product:
-        #   Kzb_b = H / s + Kzj^-1 H_b = ((I - P) / s) H,   Kzz_b += (1/s) P HHt.
+        #   Kzb_b = H / s + Kzj^-1 H_b = ((I - P) / s) H = (W Kzj^-1) Kzb,  Kzz_b += (1/s) P HHt.
         AH = linalg.gemm(HHt, A) if self.trace_adjoint else linalg.gemm(A, HHt)
-        QA = linalg.gemm(Kp_inv, A)
+        _wait(main, mat)
         A_b = _lincomb([(AH, -1.0, -1), (QA, -w, 0)], s)
-        P = linalg.gemm(Kzj_inv, Q)
         PHH = linalg.gemm(P, HHt)
-        W = _lincomb([(P, -1.0, -1)], s, diag=(1.0, -1))  # (I - P) / s
-        Kzb_b = linalg.gemm(W, H)
-        qv = linalg.gemm(Kp_inv, _col(m)).reshape(-1)
-        m_b = _lincomb([(u, 1.0, 0), (qv, -w, 0)])
-        QAQA = linalg.gemm(QA, QA, transb=True)
+        Kzb_b = linalg.gemm(linalg.gemm(W, Kzj_inv), Kzb)
         LiLi = st["LiLi"] if "LiLi" in st else _spd_inv(Li)
-        t_b = linalg.gemm(Kzz, _col(m_b)) / s
-        c_b = linalg.gemm(Li, linalg.gemm(Li, t_b, tri_a=True), transa=True, tri_a=True).reshape(-1)
         LiA = linalg.gemm(Li, A_b, transa=True, tri_a=True)
         # Cholesky adjoint: L^T Lbar = -A_b A^T  ->  sym(L^-T Phi(-A_b A^T) L^-1); Phi's lower
         # triangle (halved diagonal) is read through tri_a, its upper part is ignored
         Pm = _lincomb([(linalg.gemm(A_b, A, transb=True), -1.0, 0)], diag_scale=0.5)
         Sc = linalg.gemm(Li, linalg.gemm(Pm, Li, tri_a=True, tri_b=True), transa=True, tri_a=True)
+        _wait(main, tail)
+        tail = self._tail if use & 4 else main
         KzzS = torch.empty((M, M), dtype=F64, device=dev)
         G = torch.empty((M, M), dtype=F64, device=dev)
         call("vgposp_vgp_kzz_bar", M, _ptrs([u, v, qv, m_b, st["t"], c_b]),
              _ptrs([HHt, PHH, Kp_inv, QAQA, Kzz_inv, LiLi, Sc, LiA]), _p(s), w, _p(KzzS), _p(G),
              _stream())
+        # The two small kernel VJPs and every reduction of the loss read nothing the big product
+        # below writes: with side streams on (bit 4) they run beside it.  Every tensor they read
+        # was made on the main stream before the fork and stays referenced until the join.
+        _wait(tail, main)
+        with torch.cuda.stream(tail):
+            g1, Zb1 = kernel_vjp(self.kind, Z, Z, a, l, KzzS)
+            g3, Zb3 = kernel_vjp(self.kind, Z, Xb, a, l, Kzb_b, v, mu_b)
+            rev = [(Kp_inv, M + 1, None, 0, M, 0), (qv, 1, qv, 1, M, 0),
+                   (QAQA, M + 1, None, 0, M, 0), (m_b, 1, m, 1, M, 0), (G, 1, P0, 1, M * M, 0)]
+            _dots(fwd + rev, sums)
         # Kzx_bar = G Kzx + c_b y^T, G = (2 / s) Sinv_b (rank-1 term fused into the VJP).  A GEMM
         # whose epilogue reduced each tile straight into the VJP partials (Kzx_bar never written)
         # was measured slower: 2.92 ms against 2.30 + 0.43 ms for the two passes
@@ -344,11 +400,7 @@ class VGPObjective:
             red = torch.cat([g2, Zb2.reshape(-1)])
             self._allreduce(red)
             g2, Zb2 = red[:2], red[2:].view_as(Z)
-        g1, Zb1 = kernel_vjp(self.kind, Z, Z, a, l, KzzS)
-        g3, Zb3 = kernel_vjp(self.kind, Z, Xb, a, l, Kzb_b, v, mu_b)
-        rev = [(Kp_inv, M + 1, None, 0, M, 0), (qv, 1, qv, 1, M, 0), (QAQA, M + 1, None, 0, M, 0),
-               (m_b, 1, m, 1, M, 0), (G, 1, P0, 1, M * M, 0)]
-        _dots(fwd + rev, sums)
+        _wait(main, tail)
         out = torch.empty(4, dtype=F64, device=dev)
         call("vgposp_vgp_scalars", _p(sums), _p(s), _p(a), _p(g1), _p(g2), _p(g3), float(nb),
              float(M), w, j, _p(out), _stream())
