@@ -592,6 +592,22 @@ int vgposp_adam_update(double* theta, const double* grad, double* m, double* v, 
                        double lr, double beta1, double beta2, double eps, int64_t* step,
                        double grad_scale, void* stream);
 
+/* Softplus-constrained parameters (the reference's `softplus(var)` / `1e-5 + softplus(var)`
+ * kernel amplitude, length scale and noise, variational_Gaussian_process_example.py:47-61;
+ * gp_functions.py:131-134) whose unconstrained vars live in theta:
+ *   vgposp_softplus_values:       out[k] = offsets[k] + softplus(theta[slots[k]]), nparam <= 4;
+ *   vgposp_adam_update_softplus:  vgposp_adam_update where the gradient of theta[slots[k]] is
+ *                                 *gsrc[k] * sigmoid(theta[slots[k]]) (gsrc: nparam device
+ *                                 pointers; the chain rule through the softplus; grad[slots[k]]
+ *                                 is not read).
+ * One launch each instead of a few elementwise launches per parameter. */
+int vgposp_softplus_values(const double* theta, int64_t n, int nparam, const int* slots,
+                           const double* offsets, double* out, void* stream);
+int vgposp_adam_update_softplus(double* theta, const double* grad, double* m, double* v,
+                                int64_t n, double lr, double beta1, double beta2, double eps,
+                                int64_t* step, double grad_scale, int nparam, const int* slots,
+                                const double* const* gsrc, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Optional per-launch timing (no reference counterpart; the reference times with wall clocks,
  * placement_algorithm2.py:416-430).  When enabled, every launch of the library's named kernels

@@ -159,6 +159,12 @@ SIGNATURES = {
                              + [ctypes.POINTER(_c_void_p)] * 6),
     "vgposp_adam_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64, _f64,
                                   _f64, _f64, _c_void_p, _f64, _c_void_p]),
+    "vgposp_softplus_values": (_i32, [_c_void_p, _i64, _i32, ctypes.POINTER(_i32),
+                                      ctypes.POINTER(_f64), _c_void_p, _c_void_p]),
+    "vgposp_adam_update_softplus": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f64,
+                                           _f64, _f64, _f64, _c_void_p, _f64, _i32,
+                                           ctypes.POINTER(_i32), ctypes.POINTER(_c_void_p),
+                                           _c_void_p]),
     "vgposp_prof_enable": (_i32, [_i32]),
     "vgposp_prof_dump": (_i64, [ctypes.c_char_p, _size]),
     "vgposp_prof_query": (_i32, [ctypes.c_char_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64),

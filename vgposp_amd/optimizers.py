@@ -183,22 +183,45 @@ class VGPTrainOp:
         self._g = None  # (graph, feed shapes, static X, static y, loss, statuses)
         self._hstat = None    # two pinned host buffers for the replayed steps' statuses
         self._pending = None  # (event, buffer) of the last replayed step, not yet checked
+        self._pv = None       # the three softplus parameter values (one launch per step)
 
     def _value(self, p):
         return resolve(p).reshape(())
 
     def _step(self, Xb, yb, infos=None):
         Zv = self.Z.value if isinstance(self.Z, Variable) else linalg.as_device(self.Z)
+        names = ("amp", "ls", "noise")
+        fused = os.environ.get("VGPOSP_FUSED_PARAMS", "1") != "0"  # A/B switch
+        if fused and all(k in self.slot for k in names):
+            # all three are trainable softplus parameters in theta: their values in one launch,
+            # their softplus chain rule inside the Adam launch
+            if self._pv is None:
+                self._pv = torch.empty(3, dtype=torch.float64, device=self.theta.device)
+            slots = (ctypes.c_int * 3)(*[self.slot[k] for k in names])
+            call("vgposp_softplus_values", ctypes.c_void_p(self.theta.data_ptr()),
+                 self.theta.numel(), 3, slots,
+                 (ctypes.c_double * 3)(*[float(self.params[k].offset) for k in names]),
+                 ctypes.c_void_p(self._pv.data_ptr()), linalg._stream())
+            vals = [self._pv[i] for i in range(3)]
+        else:
+            vals = [self._value(self.params[k]) for k in names]
+        zbar = self.grad[self.z_off:].view_as(Zv) if self.train_Z else None
         loss, ga, gl, gn, gZ = self.objective.loss_and_grads(
-            Zv, self._value(self.params["amp"]), self._value(self.params["ls"]),
-            self._value(self.params["noise"]), Xb, yb, self.loss.kl_weight, infos=infos)
-        for k, g in (("amp", ga), ("ls", gl), ("noise", gn)):
-            if k in self.slot:
-                i = self.slot[k]
+            Zv, *vals, Xb, yb, self.loss.kl_weight, infos=infos, zbar_out=zbar)
+        chain = [(self.slot[k], g) for k, g in zip(names, (ga, gl, gn)) if k in self.slot]
+        if not fused:  # the chain rule as elementwise launches (A/B reference)
+            for i, g in chain:
+                k = names[[self.slot.get(n) for n in names].index(i)]
                 self.grad[i:i + 1] = g * self.params[k].dvalue_dvar().reshape(-1)
-        if self.train_Z:
+            chain = []
+        if self.train_Z and gZ is not zbar:
             self.grad[self.z_off:] = gZ.reshape(-1)
-        _adam(self.theta, self.grad, self.m, self.v, self.step_count, self.opt, 1.0)
+        call("vgposp_adam_update_softplus", ctypes.c_void_p(self.theta.data_ptr()),
+             ctypes.c_void_p(self.grad.data_ptr()), ctypes.c_void_p(self.m.data_ptr()),
+             ctypes.c_void_p(self.v.data_ptr()), self.theta.numel(), self.opt.lr, self.opt.beta1,
+             self.opt.beta2, self.opt.epsilon, ctypes.c_void_p(self.step_count.data_ptr()), 1.0,
+             len(chain), (ctypes.c_int * 4)(*[i for i, _ in chain]),
+             (ctypes.c_void_p * 4)(*[g.data_ptr() for _, g in chain]), linalg._stream())
         return loss
 
     def _replay(self, Xb, yb):

@@ -265,8 +265,10 @@ class VGPObjective:
             st.update(fac[0])
         return st
 
-    def loss_and_grads(self, Z, amp, ls, noise, Xb, yb, kl_weight, want_grads=True, infos=None):
-        """-> (loss, d/damp, d/dls, d/dnoise, d/dZ [M, d]) as 0-d / [M, d] device tensors.
+    def loss_and_grads(self, Z, amp, ls, noise, Xb, yb, kl_weight, want_grads=True, infos=None,
+                       zbar_out=None):
+        """-> (loss, d/damp, d/dls, d/dnoise, d/dZ [M, d]) as 0-d / [M, d] device tensors
+        (d/dZ written into ``zbar_out`` when given).
 
         No host synchronisation unless ``infos`` is None: with a list, the device Cholesky
         statuses are appended for the caller to check (the graph-captured training step)."""
@@ -404,7 +406,7 @@ class VGPObjective:
         out = torch.empty(4, dtype=F64, device=dev)
         call("vgposp_vgp_scalars", _p(sums), _p(s), _p(a), _p(g1), _p(g2), _p(g3), float(nb),
              float(M), w, j, _p(out), _stream())
-        Z_b = _lincomb([(Zb1, -1.0, 0), (Zb2, -1.0, 0), (Zb3, -1.0, 0)])
+        Z_b = _lincomb([(Zb1, -1.0, 0), (Zb2, -1.0, 0), (Zb3, -1.0, 0)], out=zbar_out)
         if check:
             for info in infos:
                 linalg.check_info(info)
