@@ -112,6 +112,18 @@ int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, int64_t k, 
                        double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int splits,
                        void* ws, size_t ws_bytes, void* stream);
 
+/* Grouped vgposp_gemm: `count` independent products, problem g with flags[5g..5g+4] = (transa,
+ * transb, uplo_c, tri_a, tri_b), dims[3g..3g+2] = (m, n, k), alpha[g], beta[g], A[g] (lda[g]),
+ * B[g] (ldb[g]), C[g] (ldc[g]), all in ONE launch (problem on blockIdx.y) plus one grouped split-K
+ * reduction; problems the MFMA tile kernel does not take (n == 1, odd or unaligned operands) run
+ * one by one.  For the VGP step's latency-bound M x M products.  ws holds
+ * vgposp_gemm_group_workspace_bytes(count, flags, dims) bytes of split-K partials. */
+size_t vgposp_gemm_group_workspace_bytes(int count, const int* flags, const int64_t* dims);
+int vgposp_gemm_group(int count, const int* flags, const int64_t* dims, const double* alpha,
+                      const double* beta, const double* const* A, const int64_t* lda,
+                      const double* const* B, const int64_t* ldb, double* const* C,
+                      const int64_t* ldc, void* ws, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * VGP training-step glue (vgposp_amd/vgp_training.py): the non-GEMM element-wise and reduction
  * parts of variational_loss and of the gradient TF autodiff takes through it

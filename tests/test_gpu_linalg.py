@@ -327,3 +327,39 @@ def test_kernel_matrix_matvec(L, kind, n1, n2, d):
     ref = ogp.kernel_matrix(kind, X1, X2, 0.8, 0.9)[0]
     np.testing.assert_allclose(K.cpu().numpy(), ref, rtol=1e-13, atol=1e-300)
     np.testing.assert_allclose(out.cpu().numpy(), ref @ v, rtol=1e-11, atol=1e-12)
+
+
+# (ta, tb, tri_a, tri_b, lower, m, n, k): every flag the grouped kernel dispatches on, shapes that
+# split (512^3), that do not (long tiles), odd / GEMV ones that fall back to single launches
+GROUP_CASES = [(0, 0, 0, 0, 0, 512, 512, 512), (1, 0, 0, 0, 0, 512, 512, 512),
+               (0, 0, 1, 0, 0, 512, 384, 512), (0, 1, 0, 0, 1, 256, 256, 1024),
+               (1, 0, 1, 1, 0, 384, 384, 384), (0, 0, 0, 1, 0, 130, 256, 256),
+               (1, 1, 0, 0, 0, 64, 96, 2048), (0, 0, 0, 0, 0, 129, 1, 77)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [0, 1])
+def test_gemm_group_matches_numpy(L, order):
+    cases = GROUP_CASES if order == 0 else GROUP_CASES[::-1]
+    rng = np.random.default_rng(11 + order)
+    specs, refs, C0s = [], [], []
+    for ta, tb, tri_a, tri_b, lower, m, n, k in cases:
+        A = rng.standard_normal((k, m) if ta else (m, k))
+        B = rng.standard_normal((n, k) if tb else (k, n))
+        C0 = rng.standard_normal((m, n))
+        opA = np.tril(A).T if (tri_a and ta) else np.tril(A) if tri_a else (A.T if ta else A)
+        opB = np.tril(B).T if (tri_b and tb) else np.tril(B) if tri_b else (B.T if tb else B)
+        refs.append(0.5 * opA @ opB - C0)
+        C0s.append(C0)
+        specs.append(dict(A=A, B=B, C=L.as_device(C0.copy()), alpha=0.5, beta=-1.0,
+                          transa=bool(ta), transb=bool(tb), lower_c=bool(lower),
+                          tri_a=bool(tri_a), tri_b=bool(tri_b)))
+    outs = L.gemm_group(specs)
+    for (ta, tb, tri_a, tri_b, lower, m, n, k), C, ref, C0 in zip(cases, outs, refs, C0s):
+        Ch = C.cpu().numpy()
+        if lower:
+            il = np.tril_indices(m)
+            np.testing.assert_allclose(Ch[il], ref[il], rtol=1e-11, atol=1e-10)
+            np.testing.assert_array_equal(Ch[np.triu_indices(m, 1)], C0[np.triu_indices(m, 1)])
+        else:
+            np.testing.assert_allclose(Ch, ref, rtol=1e-11, atol=1e-10)

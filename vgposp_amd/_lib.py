@@ -165,6 +165,14 @@ SIGNATURES = {
                                            _f64, _f64, _f64, _c_void_p, _f64, _i32,
                                            ctypes.POINTER(_i32), ctypes.POINTER(_c_void_p),
                                            _c_void_p]),
+    "vgposp_gemm_group_workspace_bytes": (_size, [_i32, ctypes.POINTER(_i32),
+                                                 ctypes.POINTER(_i64)]),
+    "vgposp_gemm_group": (_i32, [_i32, ctypes.POINTER(_i32), ctypes.POINTER(_i64),
+                                 ctypes.POINTER(_f64), ctypes.POINTER(_f64),
+                                 ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64),
+                                 ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64),
+                                 ctypes.POINTER(_c_void_p), ctypes.POINTER(_i64), _c_void_p,
+                                 _size, _c_void_p]),
     "vgposp_prof_enable": (_i32, [_i32]),
     "vgposp_prof_dump": (_i64, [ctypes.c_char_p, _size]),
     "vgposp_prof_query": (_i32, [ctypes.c_char_p, ctypes.POINTER(_f64), ctypes.POINTER(_i64),

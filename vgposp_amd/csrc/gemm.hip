@@ -387,9 +387,18 @@ template <int CFG> struct GemmCfg {
   static constexpr int OCC = VGPOSP_GEMM_OCC;  // workgroups per CU (launch bound)
 };
 
+// LDS of one workgroup of the fast kernel (doubles): the STAGES-deep ring of A sub-tiles | B.
+template <int CFG>
+constexpr int glds_smem_elems() {
+  return GemmCfg<CFG>::NST * (GemmCfg<CFG>::NSUB + 1) * OPND_ELEMS;
+}
+
+// One workgroup of the fast kernel: workgroup `bid` of the launch's `nwg` for this problem, batch
+// element bz, LDS ring at smem (the kernel's own __shared__ array).
 template <bool TA, bool TB, bool TRIA, bool TRIB, int CFG>
-__global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm_glds_kernel(
-    GemmParams p, int tiles_m, int tiles_n) {
+__device__ __forceinline__ void gemm_glds_body(const GemmParams& p, int tiles_m, int tiles_n,
+                                               const int bid, const int nwg, const int64_t bz,
+                                               double* smem) {
   if (p.abort != nullptr && *p.abort != 0) return;
   constexpr bool A_KC = !TA;
   constexpr bool B_KC = TB;
@@ -402,13 +411,12 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   constexpr int PPW = PO * (NSUB + 1);                 // pieces per wave per stage (8, 12 or 6)
   constexpr bool SPREAD = NST >= 3 || SPREAD2 > 0;     // next-tile loads between the MFMAs
   constexpr bool A_IL = false, B_IL = false;  // plain fragment order
-  __shared__ __attribute__((aligned(16))) double smem[NST * SE];
+  static_assert(NST * SE == glds_smem_elems<CFG>(), "LDS ring size");
 
   // Tile order.  Uniform-K launches: XCD-aware bijective remap (each XCD walks a contiguous range
   // of tiles, so neighbours share A rows / B columns in its L2).  A lower-triangular A (K range
   // grows with the row tile) must NOT hand contiguous ranges to XCDs — one XCD would get every
   // long tile — so it keeps the round-robin dispatch and walks row groups longest first.
-  const int nwg = gridDim.x, bid = blockIdx.x;
   int wg = bid;
   if (!TRIA) {
     const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
@@ -434,7 +442,6 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
     if (TRIA && !TA) ti = tiles_m - 1 - ti;  // longest K ranges first
   }
   const int64_t m0 = (int64_t)ti * TBM, n0 = (int64_t)tj * GBN;
-  const int64_t bz = blockIdx.y;  // batch element
   const double* const gA = p.A + bz * p.sA;
   const double* const gB = p.B + bz * p.sB;
 
@@ -683,6 +690,45 @@ __global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm
   }
 }
 
+template <bool TA, bool TB, bool TRIA, bool TRIB, int CFG>
+__global__ __launch_bounds__(64 * GemmCfg<CFG>::NW, GemmCfg<CFG>::OCC) void gemm_glds_kernel(
+    GemmParams p, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) double smem[glds_smem_elems<CFG>()];
+  gemm_glds_body<TA, TB, TRIA, TRIB, CFG>(p, tiles_m, tiles_n, blockIdx.x, gridDim.x, blockIdx.y,
+                                          smem);
+}
+
+// Grouped launch: up to GROUP_MAX independent problems (each its own shape, operands, flags and
+// split-K) in ONE launch, problem g on blockIdx.y.  For the latency-bound M x M products of the
+// VGP step, which each fill a few dozen CUs: one launch instead of one per product.
+constexpr int GROUP_MAX = 8;
+struct GemmGroup {
+  GemmParams p[GROUP_MAX];
+  int tiles_m[GROUP_MAX], tiles_n[GROUP_MAX], nwg[GROUP_MAX];
+  int flags[GROUP_MAX];  // bit 0 transa, 1 transb, 2 tri_a, 3 tri_b
+};
+
+__global__ __launch_bounds__(256, 2) void gemm_group_kernel(GemmGroup gg) {
+  __shared__ __attribute__((aligned(16))) double smem[glds_smem_elems<1>()];
+  const int g = blockIdx.y;
+  const int bid = blockIdx.x, nwg = gg.nwg[g];
+  if (bid >= nwg) return;
+  const GemmParams& p = gg.p[g];
+  const int tm = gg.tiles_m[g], tn = gg.tiles_n[g];
+#define VG_GROUP_CASE(F)                                                                         \
+  case F:                                                                                      \
+    gemm_glds_body<(F & 1) != 0, (F & 2) != 0, (F & 4) != 0, (F & 8) != 0, 1>(p, tm, tn, bid,   \
+                                                                             nwg, 0, smem);    \
+    break;
+  switch (gg.flags[g]) {
+    VG_GROUP_CASE(0) VG_GROUP_CASE(1) VG_GROUP_CASE(2) VG_GROUP_CASE(3)
+    VG_GROUP_CASE(4) VG_GROUP_CASE(5) VG_GROUP_CASE(6) VG_GROUP_CASE(7)
+    VG_GROUP_CASE(8) VG_GROUP_CASE(9) VG_GROUP_CASE(10) VG_GROUP_CASE(11)
+    VG_GROUP_CASE(12) VG_GROUP_CASE(13) VG_GROUP_CASE(14) VG_GROUP_CASE(15)
+  }
+#undef VG_GROUP_CASE
+}
+
 template <int CFG, bool TA, bool TB, bool TRIA, bool TRIB>
 static void launch_one(dim3 g1, hipStream_t stream, const GemmParams& p, int tm, int tn) {
   hipLaunchKernelGGL((gemm_glds_kernel<TA, TB, TRIA, TRIB, CFG>), g1, dim3(64 * GemmCfg<CFG>::NW),
@@ -725,6 +771,30 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(int64_t m, int6
   for (int z = 0; z < nsplit; ++z) v += part[(int64_t)z * m * n + e];
   double* c = C + row * ldc + col;
   if (beta != 0.0) v += beta * *c;
+  *c = v;
+}
+
+// The split-K reduction of a grouped launch: problem g on blockIdx.y (no-op where unsplit).
+struct ReduceGroup {
+  int64_t m[GROUP_MAX], n[GROUP_MAX], ldc[GROUP_MAX];
+  const double* part[GROUP_MAX];
+  double* C[GROUP_MAX];
+  double beta[GROUP_MAX];
+  int nsplit[GROUP_MAX], lower[GROUP_MAX];
+};
+
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_group_kernel(ReduceGroup r) {
+  const int g = blockIdx.y;
+  if (r.nsplit[g] <= 1) return;
+  const int64_t m = r.m[g], n = r.n[g];
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= m * n) return;
+  const int64_t row = e / n, col = e - row * n;
+  if (r.lower[g] && col > row) return;
+  double v = 0.0;
+  for (int z = 0; z < r.nsplit[g]; ++z) v += r.part[g][(int64_t)z * m * n + e];
+  double* c = r.C[g] + row * r.ldc[g] + col;
+  if (r.beta[g] != 0.0) v += r.beta[g] * *c;
   *c = v;
 }
 
@@ -951,6 +1021,87 @@ static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa =
   return (int)std::max<int64_t>(s, 1);
 }
 
+// Partial elements problem g of a group needs (0 when it runs unsplit or off the fast kernel).
+static int64_t group_part_elems(int transa, int64_t m, int64_t n, int64_t k, int uplo_c) {
+  if (m <= 0 || n <= 0 || k <= 0 || n == 1) return 0;
+  const int sp = auto_splits(m, n, k, uplo_c, transa);
+  return sp > 1 ? (int64_t)sp * m * n : 0;
+}
+
+// `count` independent GEMMs (flags[5 g ..]: transa, transb, uplo_c, tri_a, tri_b; dims[3 g ..]:
+// m, n, k): every problem the fast kernel takes runs in ONE grouped launch (+ one grouped split-K
+// reduction), the others (GEMV shapes, unaligned or odd operands) one by one.
+int gemm_launch_group(int count, const int* flags, const int64_t* dims, const double* alpha,
+                      const double* beta, const double* const* A, const int64_t* lda,
+                      const double* const* B, const int64_t* ldb, double* const* C,
+                      const int64_t* ldc, double* part, hipStream_t s) {
+  GemmGroup gg{};
+  ReduceGroup rg{};
+  int ng = 0, maxwg = 0;
+  int64_t poff = 0, maxel = 0;
+  double fl = 0.0, by = 0.0;
+  for (int g = 0; g < count; ++g) {
+    const int ta = flags[5 * g], tb = flags[5 * g + 1], up = flags[5 * g + 2];
+    const int tra = flags[5 * g + 3], trb = flags[5 * g + 4];
+    const int64_t m = dims[3 * g], n = dims[3 * g + 1], k = dims[3 * g + 2];
+    if (m <= 0 || n <= 0) continue;
+    const bool fast = n > 1 && k > 0 && aligned16(A[g], lda[g]) && aligned16(B[g], ldb[g]) &&
+                      m % 2 == 0 && n % 2 == 0 && k % 2 == 0 && ng < GROUP_MAX;
+    const int64_t pe = group_part_elems(ta, m, n, k, up);
+    if (!fast) {
+      if (int rc = gemm_launch_split(ta, tb, m, n, k, alpha[g], A[g], lda[g], B[g], ldb[g], beta[g],
+                                     C[g], ldc[g], up, tra, trb, pe > 0 ? (int)(pe / (m * n)) : 1,
+                                     pe > 0 ? part + poff : nullptr, s))
+        return rc;
+      poff += pe;
+      continue;
+    }
+    GemmParams p{m, n, k, alpha[g], beta[g], A[g], lda[g], B[g], ldb[g], C[g], ldc[g], up, tra, trb,
+                 1, 0, 0, nullptr, 0, 0, 0, 0, tl_gemm_abort};
+    const int tm = (int)ceil_div(m, GBM), tn = (int)ceil_div(n, GBN);
+    const int64_t nblk = up == VGPOSP_LOWER ? (int64_t)tm * (tm + 1) / 2 : (int64_t)tm * tn;
+    if (pe > 0) {
+      const int sp = (int)(pe / (m * n));
+      p.nblk = (int)nblk;
+      p.kchunk = ceil_div(ceil_div(k, sp), GBK) * GBK;
+      p.nsplit = (int)ceil_div(k, p.kchunk);
+      p.part = part + poff;
+      poff += pe;
+    }
+    const double outs = up == VGPOSP_LOWER ? 0.5 * (double)m * (double)(m + 1) : (double)m * n;
+    fl += 2.0 * (double)k * outs * ((tra && trb) ? (1.0 / 3.0) : (tra || trb) ? 0.5 : 1.0);
+    by += 8.0 * ((double)m * k + (double)k * n + (beta[g] != 0.0 ? 2.0 : 1.0) * outs);
+    gg.p[ng] = p;
+    gg.tiles_m[ng] = tm;
+    gg.tiles_n[ng] = tn;
+    gg.nwg[ng] = (int)(nblk * p.nsplit);
+    gg.flags[ng] = (ta ? 1 : 0) | (tb ? 2 : 0) | (tra ? 4 : 0) | (trb ? 8 : 0);
+    maxwg = std::max(maxwg, gg.nwg[ng]);
+    rg.m[ng] = m;
+    rg.n[ng] = n;
+    rg.ldc[ng] = ldc[g];
+    rg.part[ng] = p.part;
+    rg.C[ng] = C[g];
+    rg.beta[ng] = beta[g];
+    rg.nsplit[ng] = p.nsplit;
+    rg.lower[ng] = up == VGPOSP_LOWER;
+    if (p.nsplit > 1) maxel = std::max(maxel, m * n);
+    ++ng;
+  }
+  if (ng == 0) return 0;
+  {
+    ProfScope ps("gemm_f64", s, fl, by);
+    hipLaunchKernelGGL(gemm_group_kernel, dim3((unsigned)maxwg, (unsigned)ng), dim3(256), 0, s, gg);
+    VG_LAUNCH_CHECK();
+  }
+  if (maxel > 0) {
+    hipLaunchKernelGGL(gemm_splitk_reduce_group_kernel, dim3((unsigned)ceil_div(maxel, 256), (unsigned)ng),
+                       dim3(256), 0, s, rg);
+    VG_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
 void gemm_set_abort(const int* flag) { tl_gemm_abort = flag; }
 
 int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa) {
@@ -1052,4 +1203,50 @@ extern "C" int vgposp_gemm_batched(int transa, int transb, int64_t m, int64_t n,
   return gemm_launch_batched(transa, transb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc,
                              sC, uplo_c, tri_a, tri_b, sp, sp > 1 ? static_cast<double*>(ws) : nullptr,
                              (int64_t)sp * m * n, batch, as_stream(stream));
+}
+
+extern "C" size_t vgposp_gemm_group_workspace_bytes(int count, const int* flags,
+                                                    const int64_t* dims) {
+  using namespace vgposp;
+  if (count <= 0 || flags == nullptr || dims == nullptr) return 0;
+  int64_t el = 0;
+  for (int g = 0; g < count; ++g)
+    el += group_part_elems(flags[5 * g], dims[3 * g], dims[3 * g + 1], dims[3 * g + 2],
+                           flags[5 * g + 2]);
+  return 8 * (size_t)el;
+}
+
+extern "C" int vgposp_gemm_group(int count, const int* flags, const int64_t* dims,
+                                 const double* alpha, const double* beta, const double* const* A,
+                                 const int64_t* lda, const double* const* B, const int64_t* ldb,
+                                 double* const* C, const int64_t* ldc, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(count >= 0, 1);
+  if (count == 0) return 0;
+  VG_CHECK_ARG(flags != nullptr, 2);
+  VG_CHECK_ARG(dims != nullptr, 3);
+  VG_CHECK_ARG(alpha != nullptr && beta != nullptr, 4);
+  VG_CHECK_ARG(A != nullptr && lda != nullptr && B != nullptr && ldb != nullptr, 6);
+  VG_CHECK_ARG(C != nullptr && ldc != nullptr, 10);
+  for (int g = 0; g < count; ++g) {
+    const int ta = flags[5 * g], tb = flags[5 * g + 1], up = flags[5 * g + 2];
+    const int64_t m = dims[3 * g], n = dims[3 * g + 1], k = dims[3 * g + 2];
+    VG_CHECK_ARG(m >= 0 && n >= 0 && k >= 0, 3);
+    VG_CHECK_ARG(up == VGPOSP_FULL || (up == VGPOSP_LOWER && m == n), 2);
+    VG_CHECK_ARG(A[g] != nullptr || m == 0 || k == 0, 6);
+    VG_CHECK_ARG(lda[g] >= (ta ? (m > 0 ? m : 1) : (k > 0 ? k : 1)), 7);
+    VG_CHECK_ARG(B[g] != nullptr || n == 0 || k == 0, 8);
+    VG_CHECK_ARG(ldb[g] >= (tb ? (k > 0 ? k : 1) : (n > 0 ? n : 1)), 9);
+    VG_CHECK_ARG(C[g] != nullptr || m == 0 || n == 0, 10);
+    VG_CHECK_ARG(ldc[g] >= (n > 0 ? n : 1), 11);
+  }
+  const size_t need = vgposp_gemm_group_workspace_bytes(count, flags, dims);
+  if (need > 0 && (ws == nullptr || ws_bytes < need)) {
+    set_error("vgposp_gemm_group: workspace %zu < %zu bytes", ws_bytes, need);
+    return VGPOSP_E_WS;
+  }
+  return gemm_launch_group(count, flags, dims, alpha, beta, A, lda, B, ldb, C, ldc,
+                           static_cast<double*>(ws), as_stream(stream));
 }

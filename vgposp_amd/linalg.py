@@ -143,6 +143,55 @@ def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=
     return C
 
 
+def gemm_group(specs):
+    """Independent GEMMs in ONE launch (vgposp_gemm_group): ``specs`` is a list of dicts with the
+    arguments of :func:`gemm` (A, B and optionally C, alpha, beta, transa, transb, lower_c, tri_a,
+    tri_b).  Returns the list of C.  For latency-bound small products (each filling a few dozen
+    CUs) that a single stream would otherwise issue one after another."""
+    n = len(specs)
+    if n == 0:
+        return []
+    if os.environ.get("VGPOSP_GEMM_GROUP", "1") == "0":  # A/B: one launch per product
+        return [gemm(**sp) for sp in specs]
+    flags, dims, al, be, As, lda, Bs, ldb, Cs, ldc, outs = ([] for _ in range(11))
+    keep = []  # device copies of host operands stay alive until the launch is enqueued
+    for sp in specs:
+        A, B = as_device(sp["A"]), as_device(sp["B"])
+        keep += [A, B]
+        ta, tb = bool(sp.get("transa", False)), bool(sp.get("transb", False))
+        lower = bool(sp.get("lower_c", False))
+        m = A.shape[1] if ta else A.shape[0]
+        k = A.shape[0] if ta else A.shape[1]
+        kb = B.shape[1] if tb else B.shape[0]
+        nn = B.shape[0] if tb else B.shape[1]
+        if k != kb:
+            raise ValueError(f"gemm_group: inner dimensions differ: {k} vs {kb}")
+        C, beta = sp.get("C"), float(sp.get("beta", 0.0))
+        if C is None:
+            C = (torch.zeros if lower else torch.empty)((m, nn), dtype=F64, device=A.device)
+            beta = 0.0
+        flags += [int(ta), int(tb), LOWER if lower else FULL, int(bool(sp.get("tri_a", False))),
+                  int(bool(sp.get("tri_b", False)))]
+        dims += [m, nn, k]
+        al.append(float(sp.get("alpha", 1.0)))
+        be.append(beta)
+        As.append(A.data_ptr())
+        lda.append(A.stride(0))
+        Bs.append(B.data_ptr())
+        ldb.append(B.stride(0))
+        Cs.append(C.data_ptr())
+        ldc.append(C.stride(0))
+        outs.append(C)
+    fl = (ctypes.c_int * len(flags))(*flags)
+    dm = (ctypes.c_int64 * len(dims))(*dims)
+    ws = workspace(query("vgposp_gemm_group_workspace_bytes", n, fl, dm))
+    vp = ctypes.c_void_p
+    call("vgposp_gemm_group", n, fl, dm, (ctypes.c_double * n)(*al), (ctypes.c_double * n)(*be),
+         (vp * n)(*As), (ctypes.c_int64 * n)(*lda), (vp * n)(*Bs), (ctypes.c_int64 * n)(*ldb),
+         (vp * n)(*Cs), (ctypes.c_int64 * n)(*ldc), _p(ws), ws.numel(), _stream())
+    return outs
+
+
 def gemm_batched(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=False,
                  tri_a=False, tri_b=False):
     """C[b] = alpha op(A[b]) op(B[b]) + beta C[b] for [batch, rows, cols] contiguous operands, one

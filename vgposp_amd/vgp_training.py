@@ -150,8 +150,7 @@ class VGPObjective:
         self.group = group
         self._Kzx = None
         self._side = None
-        self._tail = None  # side streams of the step (Kzb, the vector chain, VJPs, reductions)
-        self._mat = None   # side stream of the M x M chain
+        self._tail = None  # side stream of the step (Kzb, the vector chain, VJPs, reductions)
 
     def _allreduce(self, t):
         """Sum over the data-parallel group (host-staged for gloo, in place on device for RCCL)."""
@@ -286,13 +285,14 @@ class VGPObjective:
         # assembled beside the forward posterior's Kzx assembly and SYRK
         main = torch.cuda.current_stream()
         if self._tail is None:
-            # Side streams, bit 1: Kzb beside the forward pass, 2: the three middle chains, 4:
-            # VJPs and reductions beside G Kzx.  Measured per segment (tools/vgp_ab.py,
-            # profiles/r3_vgp_ab_streams_segments_*.jsonl): the fp64 step is fastest on ONE stream
-            # (C3 6.14 ms with none, 6.19-6.28 with any; C5 7.25 against 7.40-7.54), the mixed one
-            # with all three (9.15 against 9.72 ms: its factorizations already run on side streams).
+            # Side stream use, bit 1: Kzb beside the forward pass, 2: the vector chain beside the
+            # M x M products, 4: VJPs and reductions beside G Kzx.  Measured per segment
+            # (tools/vgp_ab.py, profiles/r3_vgp_ab_streams_segments_*.jsonl): the fp64 step is
+            # fastest on ONE stream (C3 6.14 ms with none, 6.19-6.28 with any; C5 7.25 against
+            # 7.40-7.54), the mixed one with all three (9.15 against 9.72 ms: its factorizations
+            # already run on side streams).
             self._streams = int(os.environ.get("VGPOSP_VGP_STREAMS", "7" if self.mixed else "0"))
-            self._tail, self._mat = torch.cuda.Stream(), torch.cuda.Stream()
+            self._tail = torch.cuda.Stream()
         use = self._streams
         tail = self._tail if use & 1 else main
         _wait(tail, main)
@@ -306,14 +306,11 @@ class VGPObjective:
         Kzj_inv, Lpi, Kp_inv, Kzz_inv = (st[k] for k in ("Kzj_inv", "Lpi", "Kp_inv", "Kzz_inv"))
         dev = Z.device
         # ---- variational loss (every scalar is taken at the end by vgposp_dots / _scalars) ----
-        # Three independent chains until A_b: the SYRK Kzb Kzb^T and H H^T, the vector chain (v, r,
-        # u, m_b, c_b: GEMVs) and the M x M products of A; with side streams on (bit 2) the last two
-        # run on their own streams beside the first.  Every operand comes from before the fork;
-        # every result is read only after a join.
+        # The vector chain (v, r, u, m_b, c_b: GEMVs) is independent of the matrix products until
+        # the Kzz adjoint; with side streams on (bit 2) it runs on its own stream beside them.
+        # Every operand comes from before the fork; every result is read only after the join.
         tail = self._tail if use & 2 else main
-        mat = self._mat if use & 2 else main
         _wait(tail, main)
-        _wait(mat, main)
         with torch.cuda.stream(tail):
             v = linalg.gemm(Kzj_inv, _col(m))
             r = yb.clone()
@@ -328,21 +325,26 @@ class VGPObjective:
                 t_b = linalg.gemm(Kzz, _col(m_b)) / s
                 c_b = linalg.gemm(Li, linalg.gemm(Li, t_b, tri_a=True), transa=True,
                                   tri_a=True).reshape(-1)
-        with torch.cuda.stream(mat):
-            Q = linalg.gemm(A, A, transa=not self.trace_adjoint, transb=self.trace_adjoint)
-            PA = linalg.gemm(Lpi, A, tri_a=True)
-            if want_grads:
-                QA = linalg.gemm(Kp_inv, A)
-                P = linalg.gemm(Kzj_inv, Q)
-                W = _lincomb([(P, -1.0, -1)], s, diag=(1.0, -1))  # (I - P) / s
-                QAQA = linalg.gemm(QA, QA, transb=True)
         # Trace terms from ONE M x B product, the SYRK Sb = Kzb Kzb^T: with H = Kzj^-1 Kzb
         # (Kzj^-1 = Lzi^T Lzi) and R = op(A) H,  tr(G^T G) = <Kzb, H> = <Sb, Kzj^-1> for
         # G = Lzi Kzb, and tr(R^T R) = <Q, H H^T> with Q = A^T A (A A^T for the trace_adjoint
         # form) and H H^T = Kzj^-1 Sb Kzj^-1 (M x M products); H itself is never formed.
+        # The M x M products go in dependency levels, each level ONE grouped launch
+        # (linalg.gemm_group): they are latency-bound and fill only a few dozen CUs each.
         Sb = linalg.gemm(Kzb, Kzb, transb=True, lower_c=True)
         call("vgposp_sym_from_lower", _p(Sb), M, M, _stream())
-        HHt = linalg.gemm(linalg.gemm(Kzj_inv, Sb), Kzj_inv, lower_c=True)
+        ta = self.trace_adjoint
+        lv = [dict(A=Kzj_inv, B=Sb), dict(A=A, B=A, transa=not ta, transb=ta),
+              dict(A=Lpi, B=A, tri_a=True)]
+        if want_grads:
+            lv.append(dict(A=Kp_inv, B=A))
+        T1, Q, PA, *rest = linalg.gemm_group(lv)
+        HHt = torch.empty((M, M), dtype=F64, device=dev)  # lower product, then mirrored
+        lv = [dict(A=T1, B=Kzj_inv, C=HHt, lower_c=True)]
+        if want_grads:
+            QA = rest[0]
+            lv += [dict(A=Kzj_inv, B=Q), dict(A=QA, B=QA, transb=True)]
+        _, *rest = linalg.gemm_group(lv)
         call("vgposp_sym_from_lower", _p(HHt), M, M, _stream())
         sums = torch.zeros(13, dtype=F64, device=dev)  # VGPOSP_S_* of vgposp.h
         fwd = [(r, 1, r, 1, nb, 0), (Sb, 1, Kzj_inv, 1, M * M, 0), (Q, 1, HHt, 1, M * M, 0),
@@ -350,7 +352,6 @@ class VGPObjective:
                (st["ldp"], 1, None, 0, M, 1), (st["ldk"], 1, None, 0, M, 1)]
         if not want_grads:
             _wait(main, tail)
-            _wait(main, mat)
             _dots(fwd, sums)
             zero = torch.zeros(2, dtype=F64, device=dev)
             out = torch.empty(4, dtype=F64, device=dev)
@@ -360,24 +361,26 @@ class VGPObjective:
                 for info in infos:
                     linalg.check_info(info)
             return out[0], None, None, None, None
+        P, QAQA = rest
         # ---- reverse pass (d E) ----
         # dE/dR = -R / s gives A_b = -(1/s) A HHt (HHt A for trace_adjoint) and H_b = -(1/s) Q H;
         # through H = Kzj^-1 Kzb: Kzb_b += Kzj^-1 H_b, Kzz_b -= Kzj^-1 H_b H^T.  With
         # P = Kzj^-1 Q all of it is M x M work plus one M x B product:
         #   Kzb_b = H / s + Kzj^-1 H_b = ((I - P) / s) H = (W Kzj^-1) Kzb,  Kzz_b += (1/s) P HHt.
-        AH = linalg.gemm(HHt, A) if self.trace_adjoint else linalg.gemm(A, HHt)
-        _wait(main, mat)
+        AH, PHH = linalg.gemm_group([dict(A=HHt, B=A) if ta else dict(A=A, B=HHt),
+                                     dict(A=P, B=HHt)])
         A_b = _lincomb([(AH, -1.0, -1), (QA, -w, 0)], s)
-        PHH = linalg.gemm(P, HHt)
-        Kzb_b = linalg.gemm(linalg.gemm(W, Kzj_inv), Kzb)
+        W = _lincomb([(P, -1.0, -1)], s, diag=(1.0, -1))  # (I - P) / s
+        WK, LiA, ABt = linalg.gemm_group([dict(A=W, B=Kzj_inv),
+                                          dict(A=Li, B=A_b, transa=True, tri_a=True),
+                                          dict(A=A_b, B=A, transb=True)])
+        Kzb_b = linalg.gemm(WK, Kzb)
         LiLi = st["LiLi"] if "LiLi" in st else _spd_inv(Li)
-        LiA = linalg.gemm(Li, A_b, transa=True, tri_a=True)
         # Cholesky adjoint: L^T Lbar = -A_b A^T  ->  sym(L^-T Phi(-A_b A^T) L^-1); Phi's lower
         # triangle (halved diagonal) is read through tri_a, its upper part is ignored
-        Pm = _lincomb([(linalg.gemm(A_b, A, transb=True), -1.0, 0)], diag_scale=0.5)
+        Pm = _lincomb([(ABt, -1.0, 0)], diag_scale=0.5)
         Sc = linalg.gemm(Li, linalg.gemm(Pm, Li, tri_a=True, tri_b=True), transa=True, tri_a=True)
         _wait(main, tail)
-        tail = self._tail if use & 4 else main
         KzzS = torch.empty((M, M), dtype=F64, device=dev)
         G = torch.empty((M, M), dtype=F64, device=dev)
         call("vgposp_vgp_kzz_bar", M, _ptrs([u, v, qv, m_b, st["t"], c_b]),
