@@ -10,13 +10,14 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 O=$R/gpurun_out
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-ARGS="--no-cpu --no-vgp --no-potrf --no-c2 --no-c4 --no-splits --steps 1 --warmup 0"
+ARGS="--no-cpu --no-vgp --no-potrf --no-c2 --no-c4 --no-splits --no-sweep --steps 1 --warmup 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_r3 -o bench -- python3 $R/bench.py $ARGS > $O/prof_r3.log 2>&1
 python3 $R/tools/rocprof_summary.py $O/prof_r3/bench_kernel_stats.csv $O/prof_r3_summary.txt > /dev/null
 echo ok placement
-REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_r3_c4 -o c4 -- python3 $R/tools/bench_exact.py 128 50 512 > $O/prof_r3_c4.log 2>&1
-python3 $R/tools/rocprof_summary.py $O/prof_r3_c4/c4_kernel_stats.csv $O/prof_r3_c4_summary.txt 25 > /dev/null
-echo ok c4
+# C4 profile kept from the earlier run of this script
+# REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_r3_c4 -o c4 -- python3 $R/tools/bench_exact.py 128 50 512 > $O/prof_r3_c4.log 2>&1
+# python3 $R/tools/rocprof_summary.py $O/prof_r3_c4/c4_kernel_stats.csv $O/prof_r3_c4_summary.txt 25 > /dev/null
+# echo ok c4
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex 'gemm_glds|greedy_trmv|kernel_matrix' --output-format csv -d $O/pmc_r3_$c -o p -- python3 $R/bench.py $ARGS > $O/pmc_r3_$c.log 2>&1
   echo ok pmc $c
