@@ -1,0 +1,53 @@
+"""CPU: the algorithm-3 restatements are pinned to fixtures produced by the REFERENCE's arithmetic
+(tests/golden/make_golden_alg3.py: placement_algorithm2.nominator / denominator on Sigma + 1e-6 I
+minus 1e-6, argmax_cache_linear, the window loop of snippets_a3.py:43-364).
+
+* oracle.placement.sparse_placement_algorithm_3 (the pinv restatement of snippets_a3.py);
+* oracle.placement.placement_window_precision (the precision-matrix algebra the GPU uses);
+* oracle/c4_exact.c (the bounded-lazy C restatement behind the 128^3 picks), on the diagonally
+  dominant beta = 4 cases;
+* the fixture's covariance equals the tapered covariance rebuilt from its grid points, so the GPU
+  tests (tests/test_gpu_alg3_golden.py), which assemble Sigma from X, see the same input."""
+import numpy as np
+import pytest
+
+from golden_alg3 import NAMES, load
+from oracle import c4_exact as ce
+from oracle import local_placement as lpo
+from oracle import placement as op
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fixture_cov_is_tapered_cov_of_X(name):
+    m, z = load(name)
+    C = lpo.tapered_cov(z["X"], tuple(m["shape"]), m["beta"], kind=m["kernel"], ls=m["ls"],
+                        diag_shift=m["diag_shift"])
+    np.testing.assert_array_equal(C, z["cov"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_pinv_restatement_matches_reference_arithmetic(name):
+    m, z = load(name)
+    order = []
+    _, cache, dci = op.sparse_placement_algorithm_3(z["cov"], m["k"], m["shape"], m["cutoff"],
+                                                    order=order)
+    assert order == [int(a) for a in z["order"]]
+    np.testing.assert_allclose(dci, z["dci"], rtol=1e-10, atol=1e-13)
+    np.testing.assert_allclose(cache, z["cache"], rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_precision_form_matches_reference_arithmetic(name):
+    m, z = load(name)
+    order, cache, dci = op.placement_window_precision(z["cov"], m["k"], m["shape"], m["cutoff"])
+    assert [int(a) for a in order] == [int(a) for a in z["order"]]
+    np.testing.assert_allclose(dci, z["dci"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", [n for n in NAMES if load(n)[0]["beta"] >= 4.0])
+def test_c_oracle_matches_reference_arithmetic(name):
+    m, z = load(name)
+    picks, deltas = ce.exact_alg3(z["X"], m["shape"], m["k"], m["cutoff"], beta=m["beta"],
+                                  kind=m["kernel"], ls=m["ls"], diag_shift=m["diag_shift"])
+    assert [int(a) for a in picks] == [int(a) for a in z["order"]]
+    np.testing.assert_allclose(deltas, m["pick_deltas"], rtol=1e-10)
