@@ -429,50 +429,6 @@ int vgposp_greedy_buffers(void* ws, int64_t n, int kmax, double** delta, double*
                           int64_t* piv_len);
 
 /* ---------------------------------------------------------------------------------------------
- * Local-kernel greedy for grids too large for a dense cov_vv (config C4, 128^3 candidates):
- * snippets_a3.sparse_placement_algorithm_3 (snippets_a3.py:43-364) on the beta-decay tapered
- * covariance of main_architecture_2_sampledistribution.py:355-421,
- *     s(u, v) = g(|i_u - i_v|) (K(x_u, x_v) + diag_shift [u == v]),  g = tau[|i_u - i_v|^2]
- * (tau: the decay exp(-(beta d)^2 / (2 pi)) tabulated by squared index distance, 0 where < 0.01),
- * with each delta's conditioning restricted to the taper support N(y) = y + offsets (the epsilon-
- * local Hhat of snippets_a3.py:63, :182-186):
- *     nom_y   = s_yy - s_yB (S_BB + jitter I)^-1 s_By,  B = A ∩ N(y)
- *     denom_y = s_yy - s_yB (S_BB + jitter I)^-1 s_By,  B = N(y) \ A
- *     delta_y = 0 if |nom| or |denom| < threshold (snippets_a2.py:480) else nom / denom.
- * K is evaluated from X on the fly; nothing N x N exists.  Common arguments (VGPOSP_LOCAL_ARGS):
- *   X: [I0*I1*I2][3] C-order grid points (replicated on every rank); amp, ls: the kernel's;
- *   offsets: [m-1][3] int32 device, the support without 0 in C order, m <= 64; tau: [ntau]
- *   device, the decay by squared index distance; selected: uint8 [N] device mask of A
- *   (replicated); the rank owns the candidate slab [c0, c1) and its cache[y - c0] (the
- *   reference's delta_cached); cutoff: the re-score window [i_d - cutoff, i_d + cutoff) per axis
- *   (snippets_a3.py:190-303); info: device int32, set to 1 when a conditioning block is not
- *   positive definite; ws: vgposp_local_workspace_bytes(c1 - c0) (per-block arg-max keys).
- *   vgposp_local_score:  every candidate of the slab (round 0, snippets_a3.py:77-124) + block keys.
- *   vgposp_local_select: after round `round - 1`'s pick and window, refresh the touched block keys
- *                        and write the slab's arg-max to key_out ([2] int64: the delta's bits, the
- *                        index; ties -> lowest index, placement_algorithm2.py:24-50).
- *   vgposp_local_pick:   y* = the best of nkeys gathered keys (the candidate-sharded arg-max: the
- *                        ranks all-gather their 16-byte keys, RCCL over xGMI); marks it selected,
- *                        picks[round] = y*, pick_delta[round] = its delta, cache[y*] = 0 on the
- *                        owner (snippets_a3.py:162-168), then (do_window) re-scores its window.
- *   vgposp_local_run:    single rank: the full pass and all k rounds (one persistent workgroup for
- *                        the rounds when m <= 16).  keys: [2] int64 device scratch.
- * --------------------------------------------------------------------------------------------- */
-#define VGPOSP_LOCAL_ARGS                                                                         \
-  int kind, const double *X, int64_t I0, int64_t I1, int64_t I2, double amp, double ls,           \
-      double diag_shift, double jitter, double threshold, const int *offsets, int m,              \
-      const double *tau, int ntau, uint8_t *selected, int64_t c0, int64_t c1, int cutoff,         \
-      double *cache, int *info, void *ws, size_t ws_bytes
-size_t vgposp_local_workspace_bytes(int64_t n_local);
-int vgposp_local_score(VGPOSP_LOCAL_ARGS, void* stream);
-int vgposp_local_select(VGPOSP_LOCAL_ARGS, const int64_t* picks, int round, int64_t* key_out,
-                        void* stream);
-int vgposp_local_pick(VGPOSP_LOCAL_ARGS, const int64_t* keys, int nkeys, int round, int do_window,
-                      int64_t* picks, double* pick_delta, void* stream);
-int vgposp_local_run(VGPOSP_LOCAL_ARGS, int k, int64_t* picks, double* pick_delta, int64_t* keys,
-                     void* stream);
-
-/* ---------------------------------------------------------------------------------------------
  * Exact algorithm 3 at grid sizes where cov_vv cannot be dense (config C4, 128^3): the beta-decay
  * tapered covariance (main_architecture_2_sampledistribution.py:355-421) is a sparse SPD stencil
  * matrix, and snippets_a3.sparse_placement_algorithm_3 (snippets_a3.py:43-364) with tf_nominator /

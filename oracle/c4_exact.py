@@ -17,7 +17,7 @@ import time
 
 import numpy as np
 
-from .local_placement import TF_JITTER, TF_SMALL, taper_support
+from .taper import TF_JITTER, TF_SMALL, taper_support
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libc4oracle.so")

@@ -1,0 +1,67 @@
+"""Oracle (TEST INFRASTRUCTURE ONLY): the beta-decay tapered covariance of config C4 in numpy.
+
+* ``decay`` / ``taper_support``: the local kernel of main_architecture_2_sampledistribution.py:355-421:
+  cov(u, v) is multiplied by ``exp(-(beta * delta)^2 / (2 pi))`` (delta = Euclidean distance of the
+  C-order grid indices, ``:375-378``, ``:390-393``) and set to 0 where that decay is < 0.01
+  (``:417-420``).  With the reference's ``BETA_val = 4`` (``:779``, ``:973``) only the 6 face
+  neighbours survive.
+* ``window``: the index window ``[i_d - cutoff, i_d + cutoff)`` per axis that algorithm 3 re-scores
+  after each pick (snippets_a3.py:190-303).
+* ``tapered_cov``: the dense tapered covariance (small grids only) that the reference's algorithm 3
+  consumes; the fixtures of tests/golden/make_golden_alg3.py are built with it.
+
+The constants are the TF variant's (jitter 1e-6 on the conditioning block, snippets_a2.py:161-163;
+delta = 0 when |nom| or |denom| < 1e-7, snippets_a2.py:480; cache INF 1e8, snippets_a3.py:49).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TAPER_FLOOR = 0.01   # main_architecture_2_sampledistribution.py:392, :417
+TF_JITTER = 1e-6     # snippets_a2.py:161-163
+TF_SMALL = 1e-7      # snippets_a2.py:480
+TF_INF = 1e8         # snippets_a3.py:49
+
+
+def decay(beta, d2):
+    """main_architecture_2_sampledistribution.py:375-393 for integer squared index distances d2."""
+    delta = np.abs(np.sqrt(np.asarray(d2, dtype=np.float64)))
+    g = np.exp(-np.square(beta * delta) / (2 * np.pi))
+    return np.where(g < TAPER_FLOOR, 0.0, g)
+
+
+def taper_support(beta):
+    """(offsets [m-1, 3] int64 in lexicographic = C-order, tau[d2] table) of the taper support
+    N(0) \\ {0}: every index offset whose decay is >= 0.01."""
+    beta = float(beta)
+    r = 0
+    while decay(beta, (r + 1) ** 2) > 0:
+        r += 1
+    rng = np.arange(-r, r + 1)
+    o = np.stack(np.meshgrid(rng, rng, rng, indexing="ij"), -1).reshape(-1, 3)
+    d2 = (o ** 2).sum(1)
+    keep = (decay(beta, d2) > 0) & (d2 > 0)
+    offs = o[keep].astype(np.int64)
+    tau = decay(beta, np.arange(4 * 3 * r * r + 1))
+    return offs, tau
+
+
+def window(y, shape, cutoff):
+    """snippets_a3.py:190-303: flat indices of [i_d - cutoff, i_d + cutoff) per axis, C order."""
+    I0, I1, I2 = (int(s) for s in shape)
+    i0, r = divmod(int(y), I1 * I2)
+    i1, i2 = divmod(r, I2)
+    j0 = np.arange(max(i0 - cutoff, 0), min(i0 + cutoff, I0))
+    j1 = np.arange(max(i1 - cutoff, 0), min(i1 + cutoff, I1))
+    j2 = np.arange(max(i2 - cutoff, 0), min(i2 + cutoff, I2))
+    return ((j0[:, None, None] * I1 + j1[None, :, None]) * I2 + j2[None, None, :]).reshape(-1)
+
+
+def tapered_cov(X, shape, beta, kind="eq", amp=1.0, ls=1.0, diag_shift=0.0):
+    """The dense tapered covariance (small grids only): what the reference's arch2 filter builds
+    and its dense algorithm 3 consumes."""
+    from .covariance import index_taper
+    from .gp import kernel_matrix
+    K = kernel_matrix(kind, X, X, amp, ls)[0]
+    K[np.diag_indices(len(X))] += diag_shift
+    return index_taper(K, shape, beta)

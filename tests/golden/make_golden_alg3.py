@@ -45,7 +45,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, HERE)
 
 from make_golden import _import_reference  # noqa: E402
-from oracle import local_placement as lpo  # noqa: E402
+from oracle import taper as lpo  # noqa: E402
 from vgposp_amd.data_generation import grid_points, grid_spacing  # noqa: E402
 
 EPS = 1e-6     # snippets_a2.py:161-163

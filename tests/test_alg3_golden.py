@@ -13,7 +13,7 @@ import pytest
 
 from golden_alg3 import NAMES, load
 from oracle import c4_exact as ce
-from oracle import local_placement as lpo
+from oracle import taper as lpo
 from oracle import placement as op
 
 

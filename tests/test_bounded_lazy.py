@@ -8,10 +8,10 @@ import math
 import numpy as np
 import pytest
 
-from oracle import local_placement as lp
+from oracle import taper as lp
 from oracle import placement as op
 from vgposp_amd.data_generation import grid_points, grid_spacing
-from vgposp_amd.local_placement import taper_support
+from vgposp_amd.taper import taper_support
 from vgposp_amd.sparse_placement import bound_steps, reach_table
 
 SHIFT = 0.01 + 1e-6

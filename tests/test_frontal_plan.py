@@ -6,7 +6,7 @@ import pytest
 
 from numpy_frontal_backend import selected_inverse_diag, tapered_entry_matrix
 from vgposp_amd.data_generation import grid_points, grid_spacing
-from vgposp_amd.local_placement import taper_support
+from vgposp_amd.taper import taper_support
 from vgposp_amd.nested_dissection import FrontalTree, stencil_radius
 
 

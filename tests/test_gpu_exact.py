@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import local_placement as lp
+from oracle import taper as lp
 from oracle import placement as op
 from vgposp_amd.data_generation import grid_points, grid_spacing
 

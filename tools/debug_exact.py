@@ -1,6 +1,6 @@
 import sys, numpy as np
 sys.path.insert(0, '.')
-from oracle import local_placement as lp
+from oracle import taper as lp
 from oracle import placement as op
 from vgposp_amd.data_generation import grid_points, grid_spacing
 from vgposp_amd.sparse_placement import tapered_placement_algorithm_3

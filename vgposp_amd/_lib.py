@@ -48,10 +48,6 @@ _i32 = ctypes.c_int
 _f64 = ctypes.c_double
 _size = ctypes.c_size_t
 
-# the common leading arguments of the vgposp_local_* entry points (VGPOSP_LOCAL_ARGS)
-_LOCAL = [_i32, _c_void_p, _i64, _i64, _i64, _f64, _f64, _f64, _f64, _f64, _c_void_p, _i32,
-          _c_void_p, _i32, _c_void_p, _i64, _i64, _i32, _c_void_p, _c_void_p, _c_void_p, _size]
-
 # the common leading arguments of vgposp_exact_prepare / vgposp_exact_round
 _EXACT = [_i32, _c_void_p, _i64, _i64, _i64, _f64, _f64, _f64, _f64, _f64, _c_void_p, _i32,
           _c_void_p, _i32, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
@@ -122,12 +118,6 @@ SIGNATURES = {
     "vgposp_greedy_select_window": (_i32, [_i64, _i32, _i32, _i64, _i64, _i64, _i32, _i64, _i64,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p, _size,
                                            _c_void_p]),
-    "vgposp_local_workspace_bytes": (_size, [_i64]),
-    "vgposp_local_score": (_i32, _LOCAL + [_c_void_p]),
-    "vgposp_local_select": (_i32, _LOCAL + [_c_void_p, _i32, _c_void_p, _c_void_p]),
-    "vgposp_local_pick": (_i32, _LOCAL + [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
-                                          _c_void_p]),
-    "vgposp_local_run": (_i32, _LOCAL + [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vgposp_front_factor_workspace_bytes": (_size, [_i64, _i64, _i32]),
     "vgposp_front_assemble": (_i32, [_i32, _c_void_p, _i64, _i64, _i64, _f64, _f64, _f64, _f64,
                                      _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p,

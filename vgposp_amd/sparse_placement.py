@@ -33,7 +33,7 @@ import torch
 
 from ._lib import KERNEL_KINDS, CholeskyError, call, query
 from .linalg import _p, _stream
-from .local_placement import TF_JITTER, TF_SMALL, taper_support
+from .taper import TF_JITTER, TF_SMALL, taper_support
 from .nested_dissection import frontal_tree
 
 I32 = torch.int32
