@@ -107,6 +107,13 @@ int vgposp_gemm_batched(int transa, int transb, int64_t m, int64_t n, int64_t k,
  * (about 512 workgroups, >= 512-deep ranges).  Falls back to vgposp_gemm's kernels (no split) for
  * operands the MFMA path does not take. */
 size_t vgposp_gemm_splitk_workspace_bytes(int64_t m, int64_t n, int64_t k, int uplo_c, int splits);
+/* Process-wide tuning of the automatic split-K: a short-K split (few output tiles, K < 4096) is at
+ * least min_k deep (a multiple of 16 in [16, 4096]; default 16, measured: profiles/
+ * r4_vgp_ab_splitk_*.jsonl).  Change it only while no work that was sized under the old value
+ * is being enqueued: workspace queries (vgposp_*_workspace_bytes) and the launches that use the
+ * workspace must see the same value.  Not read from the environment. */
+int vgposp_gemm_set_split_depth(int min_k);
+int vgposp_gemm_split_depth(void);
 int vgposp_gemm_splitk(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
                        const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
                        double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b, int splits,

@@ -196,8 +196,6 @@ def test_graph_replays_match_eager(torch_dev, n):
     indexed on device, no host read between steps) give bit-identical losses to the eager step.
     n = 64 is config C3, where the 10th replay once read a corrupted status before the replay
     was synchronised (tools/repro_vgp2.py)."""
-    import os
-
     from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
     torch = torch_dev
     X, y, Z = vgp_c3_data(n=n)
@@ -207,15 +205,11 @@ def test_graph_replays_match_eager(torch_dev, n):
     idx = [torch.as_tensor(rng.integers(0, N, B), device="cuda") for _ in range(14)]
     losses = {}
     for mode in ("1", "0"):
-        os.environ["VGPOSP_GRAPH"] = mode
-        try:
-            train_op, _, xb, yb = vgp_c3_graph(X, y, Z, B)
-            Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
-            out = [train_op.run({xb: Xd[i], yb: yd[i]}) for i in idx]
-            losses[mode] = [float(v) for v in out]
-            assert bool(train_op.graph) == (mode == "1")
-        finally:
-            os.environ.pop("VGPOSP_GRAPH", None)
+        train_op, _, xb, yb = vgp_c3_graph(X, y, Z, B, graph=mode == "1")
+        Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
+        out = [train_op.run({xb: Xd[i], yb: yd[i]}) for i in idx]
+        losses[mode] = [float(v) for v in out]
+        assert bool(train_op.graph) == (mode == "1")
     assert losses["1"] == losses["0"]
 
 
@@ -224,8 +218,6 @@ def test_graph_30_replays_status(torch_dev, precision):
     """30 back-to-back replays of the captured step with no host synchronisation between them
     beyond the stream-ordered status read: every status is 0 and every loss equals the eager
     step's (verdict r2 item 2: the replay-status hazard)."""
-    import os
-
     from vgposp_amd.workloads import vgp_c3_data, vgp_c3_graph
     torch = torch_dev
     X, y, Z = vgp_c3_data(n=48, m=8, half=7.0)
@@ -235,18 +227,14 @@ def test_graph_30_replays_status(torch_dev, precision):
     idx = [torch.as_tensor(rng.integers(0, N, B), device="cuda") for _ in range(32)]
     losses = {}
     for mode in ("1", "0"):
-        os.environ["VGPOSP_GRAPH"] = mode
-        try:
-            train_op, _, xb, yb = vgp_c3_graph(X, y, Z, B, precision=precision)
-            Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
-            out = [train_op.run({xb: Xd[i], yb: yd[i]}) for i in idx]
-            losses[mode] = [float(v) for v in out]
-            train_op.check()  # the last replayed step's statuses (the others: at each next run)
-            if mode == "1":
-                assert train_op._g is not None
-                assert int(torch.count_nonzero(train_op._g[5])) == 0
-        finally:
-            os.environ.pop("VGPOSP_GRAPH", None)
+        train_op, _, xb, yb = vgp_c3_graph(X, y, Z, B, precision=precision, graph=mode == "1")
+        Xd, yd = torch.as_tensor(X, device="cuda"), torch.as_tensor(y, device="cuda")
+        out = [train_op.run({xb: Xd[i], yb: yd[i]}) for i in idx]
+        losses[mode] = [float(v) for v in out]
+        train_op.check()  # the last replayed step's statuses (the others: at each next run)
+        if mode == "1":
+            assert train_op._g is not None
+            assert int(torch.count_nonzero(train_op._g[5])) == 0
     assert losses["1"] == losses["0"]
 
 

@@ -11,8 +11,6 @@ import json
 import os
 import sys
 
-if "--shapes" in sys.argv:
-    os.environ["VGPOSP_PROF_SHAPES"] = "1"
 import time
 
 import numpy as np
@@ -31,15 +29,12 @@ def main():
     ap.add_argument("--batch", type=int, default=32768)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--shapes", action="store_true", help="per-shape GEMM / per-kernel dump")
     ap.add_argument("--c5", action="store_true", help="config C5: 65,536 x 5-D, M = 4^5, B = 8192")
     ap.add_argument("--mixed", action="store_true", help="fp32 Cholesky + fp64 refinement")
     ap.add_argument("--kernel", default="eq")
     ap.add_argument("--mixed-iters", type=int, default=None,
-                    help="fp64 refinement steps of the mixed factor (VGPOSP_MIXED_ITERS)")
+                    help="fp64 refinement steps of the mixed factor (precision 'mixed:<n>')")
     args = ap.parse_args()
-    if args.mixed_iters is not None:
-        os.environ["VGPOSP_MIXED_ITERS"] = str(args.mixed_iters)
     torch.cuda.set_device(0)
     if args.c5:
         X, y, Z = vgp_c5_data()
@@ -48,7 +43,9 @@ def main():
         X, y, Z = vgp_c3_data(args.n, args.m)
     N, B = len(X), args.batch
     train_op, loss, xb, yb = vgp_c3_graph(X, y, Z, B,
-                                          precision="mixed" if args.mixed else "fp64",
+                                          precision=("fp64" if not args.mixed else "mixed" if
+                                                     args.mixed_iters is None else
+                                                     f"mixed:{args.mixed_iters}"),
                                           kernel=args.kernel)
     rng = np.random.default_rng(1)
     Xd = torch.as_tensor(X, device="cuda")
@@ -81,11 +78,6 @@ def main():
             prof[name] = {"ms_per_step": ms / args.steps, "launches_per_step": launches / args.steps,
                           "TFLOP/s": flops / (ms * 1e-3) / 1e12 if flops else None,
                           "GB/s": nbytes / (ms * 1e-3) / 1e9}
-    if args.shapes:
-        d = _lib.prof_dump()
-        for name, (ms, n, fl, _) in sorted(d.items(), key=lambda kv: -kv[1][0])[:30]:
-            tf = fl / (ms * 1e-3) / 1e12 if fl and ms else 0.0
-            print(f"{name:44s} {ms / args.steps:8.3f} ms/step {n / args.steps:6.1f} x {tf:6.1f} TF/s")
     _lib.prof_enable(False)
     M = Z.shape[0]
     print(json.dumps({"N": N, "M": M, "batch": B, "kernel": args.kernel, "mixed": args.mixed,

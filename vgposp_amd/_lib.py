@@ -62,6 +62,8 @@ SIGNATURES = {
                                     _c_void_p]),
     "vgposp_gemm": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _c_void_p, _i64,
                            _f64, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p]),
+    "vgposp_gemm_set_split_depth": (_i32, [_i32]),
+    "vgposp_gemm_split_depth": (_i32, []),
     "vgposp_gemm_splitk_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32]),
     "vgposp_gemm_batched_workspace_bytes": (_size, [_i64, _i64, _i64, _i32, _i32]),
     "vgposp_gemm_batched": (_i32, [_i32, _i32, _i64, _i64, _i64, _f64, _c_void_p, _i64, _i64,

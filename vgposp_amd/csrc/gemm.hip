@@ -15,7 +15,7 @@
 //     MC image [k][row] with a row pitch of 144 doubles  (operand stored row-contiguous)
 // No operand ever needs an explicit transpose in HBM.
 #include <algorithm>
-#include <cstdlib>
+#include <atomic>
 #include <type_traits>
 
 #include "common.h"
@@ -998,6 +998,12 @@ int gemm_launch(int transa, int transb, int64_t m, int64_t n, int64_t k, double 
                            tri_a, tri_b, 1, nullptr, stream);
 }
 
+// Minimum depth of a short-K split (vgposp_gemm_set_split_depth).  Set explicitly by the caller,
+// never from the environment: every workspace query and the launch that uses the workspace read
+// the same value as long as the caller does not change it in between (round 3 read it from
+// the environment on every launch, while tools/vgp_ab.py rewrote it between variants).
+static std::atomic<int> g_split_min_k{16};
+
 // Split count for a launch with few output tiles and a long K: enough workgroups for 256 CUs
 // (about two per CU), each split at least 512 deep.
 static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa = 0) {
@@ -1015,8 +1021,7 @@ static int auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa =
   // C5 7.32 -> 7.26 ms, the 65k step unchanged (16.27 vs 16.30 placements/s): a split's partial
   // costs less than the serial K-steps it removes from a latency-bound chain.
   const int64_t deep = k / 512;
-  const char* env = std::getenv("VGPOSP_SPLIT_MIN_K");
-  const int64_t min_k = env ? std::max<int64_t>(16, std::atoll(env)) : (int64_t)16;
+  const int64_t min_k = g_split_min_k.load(std::memory_order_relaxed);
   s = std::min<int64_t>(s, deep >= 8 ? deep : std::min<int64_t>(8, k / min_k));
   return (int)std::max<int64_t>(s, 1);
 }
@@ -1109,6 +1114,16 @@ int gemm_auto_splits(int64_t m, int64_t n, int64_t k, int uplo_c, int transa) {
 }
 
 }  // namespace vgposp
+
+extern "C" int vgposp_gemm_set_split_depth(int min_k) {
+  using namespace vgposp;
+  clear_error();
+  VG_CHECK_ARG(min_k >= 16 && min_k <= 4096 && min_k % 16 == 0, 1);
+  g_split_min_k.store(min_k, std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int vgposp_gemm_split_depth(void) { return vgposp::g_split_min_k.load(); }
 
 extern "C" size_t vgposp_gemm_splitk_workspace_bytes(int64_t m, int64_t n, int64_t k, int uplo_c,
                                                      int splits) {

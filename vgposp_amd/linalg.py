@@ -7,7 +7,6 @@ contiguous, float64, on a ROCm device).
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 import torch
@@ -143,15 +142,16 @@ def gemm(A, B, C=None, alpha=1.0, beta=0.0, transa=False, transb=False, lower_c=
     return C
 
 
-def gemm_group(specs):
+def gemm_group(specs, grouped=True):
     """Independent GEMMs in ONE launch (vgposp_gemm_group): ``specs`` is a list of dicts with the
     arguments of :func:`gemm` (A, B and optionally C, alpha, beta, transa, transb, lower_c, tri_a,
     tri_b).  Returns the list of C.  For latency-bound small products (each filling a few dozen
-    CUs) that a single stream would otherwise issue one after another."""
+    CUs) that a single stream would otherwise issue one after another.  ``grouped=False`` issues
+    one launch per product (the A/B reference)."""
     n = len(specs)
     if n == 0:
         return []
-    if os.environ.get("VGPOSP_GEMM_GROUP", "1") == "0":  # A/B: one launch per product
+    if not grouped:
         return [gemm(**sp) for sp in specs]
     flags, dims, al, be, As, lda, Bs, ldb, Cs, ldc, outs = ([] for _ in range(11))
     keep = []  # device copies of host operands stay alive until the launch is enqueued
@@ -253,12 +253,12 @@ def cholesky_(A, invert=False, check=True, ldiag=None):
 
 def cholesky_inv_mixed(A, iters=None, check=True):
     """Mixed-precision inverse Cholesky factor of a full symmetric [n, n] A (config C5): fp32 factor
-    on the f32 matrix cores, ``iters`` fp64 refinement steps (vgposp_potrf_mixed; default 3, or
-    the environment's VGPOSP_MIXED_ITERS for experiments).  Returns
+    on the f32 matrix cores, ``iters`` fp64 refinement steps (vgposp_potrf_mixed; default 3).
+    Returns
     (L^-1 with zeros above the diagonal, diag(L) [n], info [1], resid [1] = max|X A X^T - I| of the
     last step); A is not modified."""
     if iters is None:
-        iters = int(os.environ.get("VGPOSP_MIXED_ITERS", "3"))
+        iters = 3
     A = as_device(A)
     if A.dim() != 2 or A.shape[0] != A.shape[1]:
         raise ValueError("A must be square")

@@ -13,7 +13,6 @@ copied to the host inside the loop.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -31,17 +30,21 @@ class AdamOptimizer:
         self.epsilon = float(epsilon)
         self.name = name
 
-    def minimize(self, loss, var_list=None, group=None, precision="fp64"):
+    def minimize(self, loss, var_list=None, group=None, precision="fp64", **options):
         """``loss``: ``-log_prob`` of a GaussianProcess (a ``Negated`` LogProb, see ``negate``;
         gp_functions.tf_train_gp_adam) -> ``GPTrainOp``, or a VGP ``variational_loss``
         (variational_Gaussian_process_example.py:95-102) -> ``VGPTrainOp``.  ``group``: a
         torch.distributed group over which the VGP's observations are sharded.  ``precision``
-        (VGP only): "mixed" factors the M x M matrices in fp32 with fp64 refinement (config C5)."""
+        (VGP only): "mixed" factors the M x M matrices in fp32 with fp64 refinement (config C5).
+        ``options`` (VGP only): the ``VGPTrainOp`` scheduling switches (graph, streams,
+        fused_params, grouped)."""
         from .distributions import VariationalLoss
         if isinstance(loss, Negated):
+            if options:
+                raise TypeError(f"unexpected options for a GP train op: {sorted(options)}")
             return GPTrainOp(loss.log_prob, self, var_list)
         if isinstance(loss, VariationalLoss):
-            return VGPTrainOp(loss, self, var_list, group, precision=precision)
+            return VGPTrainOp(loss, self, var_list, group, precision=precision, **options)
         raise TypeError("minimize() expects -log_prob (a Negated LogProb) or a VGP "
                         "variational_loss")
 
@@ -127,10 +130,16 @@ class VGPTrainOp:
     is captured once into a HIP graph and replayed, with the feeds copied into static buffers —
     the same fixed graph a TF1 session runs.  A replayed step's Cholesky statuses are checked
     when the next step has been issued (or by ``check()``), so a non-PD factorization raises
-    CholeskyError one ``run`` late.  Eager when ``graph=False``, ``VGPOSP_GRAPH=0``, for
-    a data-parallel ``group``, or while the library's event timing is on."""
+    CholeskyError one ``run`` late.  Eager when ``graph=False``, for a data-parallel ``group``,
+    or while the library's event timing is on.
 
-    def __init__(self, loss, opt, var_list=None, group=None, graph=True, precision="fp64"):
+    Scheduling switches (each measured, defaults = the faster setting): ``streams`` the VGP
+    step's side-stream bitmask (``VGPObjective``), ``fused_params`` the softplus values in one
+    launch and their chain rule inside the Adam launch, ``grouped`` one launch per dependency
+    level of M x M products."""
+
+    def __init__(self, loss, opt, var_list=None, group=None, graph=True, precision="fp64",
+                 streams=None, fused_params=True, grouped=True):
         from .vgp_training import VGPObjective
         vgp = loss.vgp
         spec = getattr(vgp.variational_loc, "_vgposp_posterior", None)
@@ -177,8 +186,9 @@ class VGPTrainOp:
                                       spec["observations"], jitter=vgp.jitter,
                                       posterior_jitter=spec["jitter"],
                                       trace_adjoint=vgp.trace_adjoint, group=group,
-                                      precision=precision)
-        self.graph = bool(graph) and group is None and os.environ.get("VGPOSP_GRAPH", "1") != "0"
+                                      precision=precision, streams=streams, grouped=grouped)
+        self.fused = bool(fused_params)
+        self.graph = bool(graph) and group is None
         self._runs = 0
         self._g = None  # (graph, feed shapes, static X, static y, loss, statuses)
         self._hstat = None    # two pinned host buffers for the replayed steps' statuses
@@ -191,7 +201,7 @@ class VGPTrainOp:
     def _step(self, Xb, yb, infos=None):
         Zv = self.Z.value if isinstance(self.Z, Variable) else linalg.as_device(self.Z)
         names = ("amp", "ls", "noise")
-        fused = os.environ.get("VGPOSP_FUSED_PARAMS", "1") != "0"  # A/B switch
+        fused = self.fused
         if fused and all(k in self.slot for k in names):
             # all three are trainable softplus parameters in theta: their values in one launch,
             # their softplus chain rule inside the Adam launch

@@ -29,7 +29,6 @@ replicated and never reduced.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -129,9 +128,13 @@ class VGPObjective:
     """
 
     def __init__(self, kind, X, y, jitter=1e-6, posterior_jitter=1e-6, trace_adjoint=False,
-                 group=None, precision="fp64"):
+                 group=None, precision="fp64", streams=None, grouped=True):
         # "mixed" = fp32 factor + 3 fp64 refinement steps (fp64 to rounding); "mixed:2" = two
-        # steps (|E| 1e-2 -> 1e-8: the ELBO within north_star's 1e-5 of fp64)
+        # steps (|E| 1e-2 -> 1e-8: the ELBO within north_star's 1e-5 of fp64).
+        # ``streams``: side-stream bitmask of the training step (1: Kzb beside the forward pass,
+        # 2: the vector chain beside the M x M products, 4: VJPs and reductions beside G Kzx);
+        # None = the measured default (0 for fp64, 7 for mixed, see loss_and_grads).
+        # ``grouped``: the M x M products of one dependency level in one grouped launch.
         kind_, _, steps = str(precision).partition(":")
         if kind_ not in ("fp64", "mixed") or (steps and (kind_ != "mixed" or not steps.isdigit())):
             raise ValueError(f"precision must be 'fp64', 'mixed' or 'mixed:<steps>', "
@@ -151,6 +154,10 @@ class VGPObjective:
         self._Kzx = None
         self._side = None
         self._tail = None  # side stream of the step (Kzb, the vector chain, VJPs, reductions)
+        self._streams = (7 if self.mixed else 0) if streams is None else int(streams)
+        if not 0 <= self._streams <= 7:
+            raise ValueError(f"streams must be a bitmask in [0, 7], got {streams!r}")
+        self.grouped = bool(grouped)
 
     def _allreduce(self, t):
         """Sum over the data-parallel group (host-staged for gloo, in place on device for RCCL)."""
@@ -291,7 +298,6 @@ class VGPObjective:
             # fastest on ONE stream (C3 6.14 ms with none, 6.19-6.28 with any; C5 7.25 against
             # 7.40-7.54), the mixed one with all three (9.15 against 9.72 ms: its factorizations
             # already run on side streams).
-            self._streams = int(os.environ.get("VGPOSP_VGP_STREAMS", "7" if self.mixed else "0"))
             self._tail = torch.cuda.Stream()
         use = self._streams
         tail = self._tail if use & 1 else main
@@ -338,13 +344,13 @@ class VGPObjective:
               dict(A=Lpi, B=A, tri_a=True)]
         if want_grads:
             lv.append(dict(A=Kp_inv, B=A))
-        T1, Q, PA, *rest = linalg.gemm_group(lv)
+        T1, Q, PA, *rest = linalg.gemm_group(lv, self.grouped)
         HHt = torch.empty((M, M), dtype=F64, device=dev)  # lower product, then mirrored
         lv = [dict(A=T1, B=Kzj_inv, C=HHt, lower_c=True)]
         if want_grads:
             QA = rest[0]
             lv += [dict(A=Kzj_inv, B=Q), dict(A=QA, B=QA, transb=True)]
-        _, *rest = linalg.gemm_group(lv)
+        _, *rest = linalg.gemm_group(lv, self.grouped)
         call("vgposp_sym_from_lower", _p(HHt), M, M, _stream())
         sums = torch.zeros(13, dtype=F64, device=dev)  # VGPOSP_S_* of vgposp.h
         fwd = [(r, 1, r, 1, nb, 0), (Sb, 1, Kzj_inv, 1, M * M, 0), (Q, 1, HHt, 1, M * M, 0),
@@ -368,12 +374,12 @@ class VGPObjective:
         # P = Kzj^-1 Q all of it is M x M work plus one M x B product:
         #   Kzb_b = H / s + Kzj^-1 H_b = ((I - P) / s) H = (W Kzj^-1) Kzb,  Kzz_b += (1/s) P HHt.
         AH, PHH = linalg.gemm_group([dict(A=HHt, B=A) if ta else dict(A=A, B=HHt),
-                                     dict(A=P, B=HHt)])
+                                     dict(A=P, B=HHt)], self.grouped)
         A_b = _lincomb([(AH, -1.0, -1), (QA, -w, 0)], s)
         W = _lincomb([(P, -1.0, -1)], s, diag=(1.0, -1))  # (I - P) / s
         WK, LiA, ABt = linalg.gemm_group([dict(A=W, B=Kzj_inv),
                                           dict(A=Li, B=A_b, transa=True, tri_a=True),
-                                          dict(A=A_b, B=A, transb=True)])
+                                          dict(A=A_b, B=A, transb=True)], self.grouped)
         Kzb_b = linalg.gemm(WK, Kzb)
         LiLi = st["LiLi"] if "LiLi" in st else _spd_inv(Li)
         # Cholesky adjoint: L^T Lbar = -A_b A^T  ->  sym(L^-T Phi(-A_b A^T) L^-1); Phi's lower

@@ -62,11 +62,13 @@ def c4_grid(n=128, seed=0):
     return grid_points(shape, jitter=0.05, seed=seed), shape, 2.0 * grid_spacing(shape)
 
 
-def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64", group=None, n_total=None, kernel="eq"):
+def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64", group=None, n_total=None, kernel="eq",
+                 **train_options):
     """The reference's training graph (variational_Gaussian_process_example.py:51-102) in this
     package's API -> (train_op, loss, x_batch placeholder, y_batch placeholder).  ``group``: the
     observations (X, y) are this rank's shard of ``n_total`` (data-parallel optimal posterior,
-    two all-reduces per step); every rank feeds the same minibatch."""
+    two all-reduces per step); every rank feeds the same minibatch.  ``train_options``: the
+    VGPTrainOp scheduling switches (graph, streams, fused_params, grouped)."""
     from . import distributions as tfd
     from . import psd_kernels as tfkern
     from .optimizers import AdamOptimizer
@@ -91,5 +93,5 @@ def vgp_c3_graph(X, y, Z, B, lr=0.01, precision="fp64", group=None, n_total=None
     yb = placeholder(np.float64, [B], name="y_train_batch")
     loss = vgp.variational_loss(observations=yb, observation_index_points=xb,
                                 kl_weight=float(B) / float(n_total or len(X)))
-    return (AdamOptimizer(learning_rate=lr).minimize(loss, group=group, precision=precision), loss,
-            xb, yb)
+    return (AdamOptimizer(learning_rate=lr).minimize(loss, group=group, precision=precision,
+                                                     **train_options), loss, xb, yb)
