@@ -218,6 +218,9 @@ class NumpyGreedyBackend:
     def result(self):
         return [np.int64(s) for s in self.selected], np.array(self.sel_delta), None
 
+    def snapshot_diag(self):
+        pass  # init() reads diag(S) itself
+
     # singular cov_vv (ShardedGreedyPlacement.run's jitter retry)
     def factor_ok(self, c0, c1, partitioned, check_pivots):
         if not self.ok:

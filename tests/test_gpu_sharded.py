@@ -45,6 +45,19 @@ def _worker(rank, world, port, out, partition):
                 placement_cov(name, e), e["k"], partition_inverse=partition)]
         res["grid1080"] = [int(a) for a in placement_algorithm_2_sharded(
             _grid_cov(), 12, partition_inverse=partition, dist_min=129)]
+        # bench.py's shape: the backend is built on an UNINITIALISED buffer and Sigma is filled
+        # afterwards (and refilled between runs): the pivot check must read the diagonal at
+        # factorization time, not at construction (round-3 advice)
+        from vgposp_amd.sharded_placement import HipGreedyBackend, ShardedGreedyPlacement
+        C = torch.as_tensor(_grid_cov(), device="cuda")
+        S = torch.empty_like(C).fill_(float("nan"))
+        sh = ShardedGreedyPlacement(HipGreedyBackend(S, 12), partition_inverse=partition,
+                                    dist_min=129)
+        runs = []
+        for scale in (1.0, 2.0):
+            S.copy_(C * scale)
+            runs.append([int(a) for a in sh.run(12)[0]])
+        res["empty_then_filled"] = runs
         out[rank] = res
     finally:
         dist.destroy_process_group()
@@ -62,6 +75,7 @@ def test_sharded_two_ranks_on_gpu(partition):
         for name in ["spd40", "grid654", "grid8"]:
             assert out[r][name] == CASES[name]["alg2"], (r, name)
         assert out[r]["grid1080"] == exp_grid
+        assert out[r]["empty_then_filled"] == [exp_grid, exp_grid]
 
 
 @pytest.mark.parametrize("n,c0,c1", [(3000, 0, 1024), (3000, 1024, 2048), (3000, 2048, 3000),

@@ -72,7 +72,9 @@ class HipGreedyBackend:
         from .placement_algorithm2 import GreedyPlacement
         self._src = Sigma if copy else None
         self.g = GreedyPlacement(Sigma, kmax, copy=copy, jitter=jitter)
-        self.sdiag = torch.diagonal(self.g.S).clone()
+        # diag(Sigma) for the pivot-ratio check, taken right before each factorization
+        # (snapshot_diag): Sigma may still be unassembled here (bench.py fills it per step)
+        self.sdiag = None
         self.n = self.g.n
         self.kmax = self.g.kmax
         d, p, plen = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
@@ -87,6 +89,14 @@ class HipGreedyBackend:
         self._xcol = self.g.ws[x.value - base:x.value - base + 8 * self.n].view(torch.float64)
         self._tmp = None
 
+    def snapshot_diag(self):
+        """diag(Sigma) as the factorization will see it (a device copy, no host sync)."""
+        d = torch.diagonal(self.g.S)
+        if self.sdiag is None or self.sdiag.shape != d.shape:
+            self.sdiag = d.clone()
+        else:
+            self.sdiag.copy_(d)
+
     def init(self):
         self.g.init()
 
@@ -98,17 +108,19 @@ class HipGreedyBackend:
         partitioned) and L elsewhere."""
         from .placement_algorithm2 import PIVOT_RTOL
         g = self.g
-        if int(g.info.item()) != 0:
-            return False
-        if not check_pivots:
-            return True
-        d = torch.diagonal(g.S).clone()
-        inv = torch.ones_like(d, dtype=torch.bool)
-        if partitioned:
-            inv.zero_()
-            inv[c0:c1] = True
-        lii = torch.where(inv, 1.0 / d, d)
-        return bool(torch.min(lii * lii / self.sdiag) >= PIVOT_RTOL * g.n)
+        ok = g.info.reshape(-1)[0] == 0
+        if check_pivots:
+            if self.sdiag is None:
+                raise RuntimeError("factor_ok(check_pivots=True) needs snapshot_diag() before "
+                                   "the factorization")
+            d = torch.diagonal(g.S)
+            inv = torch.ones_like(d, dtype=torch.bool)
+            if partitioned:
+                inv.zero_()
+                inv[c0:c1] = True
+            lii = torch.where(inv, 1.0 / d, d)
+            ok = ok & (torch.min(lii * lii / self.sdiag) >= PIVOT_RTOL * g.n)
+        return bool(ok.item())  # the status and the pivot ratio in ONE host read
 
     def diag_scale(self):
         return float(torch.mean(self.sdiag).abs()) or 1.0
@@ -239,6 +251,7 @@ class ShardedGreedyPlacement:
             dist.all_reduce(x, op=dist.ReduceOp.SUM, group=self.group)
 
     def _factor(self):
+        self.b.snapshot_diag()
         if self.partition and self.world > 1 and self.dist_factor:
             from .dist_cholesky import DIST_MIN, DistCholesky
             self.b.prepare()
