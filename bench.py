@@ -367,7 +367,7 @@ def c4_line(args, world, rank, barrier, maxtime):
     g.run_bounded(run.qdiag, k)
     ev[3].record()
     torch.cuda.synchronize()
-    prof = _lib.prof_dump()
+    prof = _lib.prof_fold(_lib.prof_dump())
     _lib.prof_enable(False)
     bounds_ms, gather_ms, rounds_ms = (ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]),
                                        ev[2].elapsed_time(ev[3]))
@@ -414,7 +414,7 @@ def c4_line(args, world, rank, barrier, maxtime):
         sel.greedy.run(sel.qdiag, k)
         e[2].record()
         torch.cuda.synchronize()
-        sprof = _lib.prof_dump()
+        sprof = _lib.prof_fold(_lib.prof_dump())
         _lib.prof_enable(False)
         sel.check()
         sel_ms = e[0].elapsed_time(e[1])
@@ -669,6 +669,13 @@ def main():
     torch.cuda.synchronize()
     prof = {name: _lib.prof_query(name) for name in
             ["kernel_matrix", "gemm_f64", "potrf_diag", "greedy_colsq", "greedy_trmv", "greedy_update"]}
+    # the GEMM launches by layout class (NT / NN / TN, triangular operands, narrow = < 512
+    # workgroups): per-flop rates of the step's own shapes
+    gemm_classes = {name[len("gemm_f64"):]: {
+        "ms_per_step": v[0], "launches": v[1], "tflops": v[2] / (v[0] * 1e-3) / 1e12 if v[0] else None,
+        "frac": v[2] / (v[0] * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS if v[0] else None,
+        "share_of_gemm_flops": v[2] / prof["gemm_f64"][2] if prof["gemm_f64"][2] else None}
+        for name, v in sorted(_lib.prof_dump().items()) if name.startswith("gemm_f64[")}
     _lib.prof_enable(False)
     # exact algorithmic bytes of the triangular mat-vec: rows >= a of the lower triangle of L^-1
     # over this rank's candidate columns (the library only knows the full-triangle upper bound at
@@ -802,6 +809,7 @@ def main():
         "roofline": roof,
         "roofline_hbm": hbm,
         "breakdown": breakdown,
+        "gemm_classes": gemm_classes,
         "deterministic_selection": deterministic,
         "selected_head": sel[:8],
         "selected": sel,

@@ -60,7 +60,7 @@ def main():
     torch.cuda.synchronize()
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
-    gemm = prof.get("gemm_f64", (0, 0, 0, 0))
+    gemm = _lib.prof_fold(prof).get("gemm_f64", (0, 0, 0, 0))
     out = {"n": n, "N": n ** 3, "k": k, "leaf": leaf, "setup_s": t_setup, "plan_s": run.sel.plan_s,
            "wall_ms": best[0] * 1e3, "selinv_ms": best[1], "rounds_ms": best[2],
            "placements_per_s": k / best[0], "flops_padded": run.sel.flops(),

@@ -303,6 +303,17 @@ def prof_query(name):
     return ms.value, n.value, fl.value, by.value
 
 
+def prof_fold(dump):
+    """Fold the per-class entries of a prof_dump ("gemm_f64[nt,triA]" ...) into their family
+    ("gemm_f64"): {family: (ms, launches, flops, bytes)}."""
+    out = {}
+    for name, v in dump.items():
+        fam = name.split("[", 1)[0]
+        a = out.get(fam, (0.0, 0, 0.0, 0.0))
+        out[fam] = tuple(x + y for x, y in zip(a, v))
+    return out
+
+
 def prof_dump():
     """{name: (ms, launches, flops, bytes)} of everything recorded since prof_enable."""
     fn = load().vgposp_prof_dump

@@ -78,7 +78,10 @@ extern "C" int vgposp_prof_query(const char* name, double* total_ms, int64_t* la
   int64_t cnt = 0;
   for (size_t i = 0; i < g_nrec; ++i) {
     ProfRec& r = g_recs[i];
-    if (r.name != name) continue;
+    // a name also matches its classes: "gemm_f64" covers "gemm_f64[nt,triA]" etc.
+    const size_t nl = strlen(name);
+    if (r.name != name && !(r.name.size() > nl && r.name.compare(0, nl, name) == 0 && r.name[nl] == '['))
+      continue;
     VG_HIP(hipEventSynchronize(r.stop));
     float t = 0.f;
     VG_HIP(hipEventElapsedTime(&t, r.start, r.stop));

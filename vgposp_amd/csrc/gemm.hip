@@ -900,6 +900,22 @@ static bool aligned16(const void* ptr, int64_t ld) {
   return (reinterpret_cast<uintptr_t>(ptr) % 16 == 0) && (ld % 2 == 0);
 }
 
+// "gemm_f64[nt|nn|tn|tt][,triA][,triB][,narrow]": narrow = fewer than 512 workgroups (less than
+// two per CU: the recursion's small levels, latency-bound)
+static const char* gemm_class_name(int ta, int tb, int tra, int trb, bool wide) {
+  static const char* names[32] = {
+#define VG_CLS(L, T) "gemm_f64[" L T "]", "gemm_f64[" L T ",narrow]"
+      VG_CLS("nn", ""), VG_CLS("nn", ",triA"), VG_CLS("nn", ",triB"), VG_CLS("nn", ",triA,triB"),
+      VG_CLS("nt", ""), VG_CLS("nt", ",triA"), VG_CLS("nt", ",triB"), VG_CLS("nt", ",triA,triB"),
+      VG_CLS("tn", ""), VG_CLS("tn", ",triA"), VG_CLS("tn", ",triB"), VG_CLS("tn", ",triA,triB"),
+      VG_CLS("tt", ""), VG_CLS("tt", ",triA"), VG_CLS("tt", ",triB"), VG_CLS("tt", ",triA,triB"),
+#undef VG_CLS
+  };
+  const int lay = (ta ? 2 : 0) + (tb ? 1 : 0);
+  const int tri = (tra ? 1 : 0) + (trb ? 2 : 0);
+  return names[(lay * 4 + tri) * 2 + (wide ? 0 : 1)];
+}
+
 int gemm_launch_batched(int transa, int transb, int64_t m, int64_t n, int64_t k, double alpha,
                         const double* A, int64_t lda, int64_t sA, const double* B, int64_t ldb,
                         int64_t sB, double beta, double* C, int64_t ldc, int64_t sC, int uplo_c,
@@ -958,8 +974,11 @@ int gemm_launch_batched(int transa, int transb, int64_t m, int64_t n, int64_t k,
       p.nsplit = (int)ceil_div(k, p.kchunk);
       p.part = part;
     }
-    ProfScope ps("gemm_f64", stream, fl,
-                 8.0 * batch * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs));
+    const double by =
+        8.0 * batch * ((double)m * k + (double)k * n + (beta != 0.0 ? 2.0 : 1.0) * outs);
+    // recorded under its layout class; vgposp_prof_query("gemm_f64") sums the classes
+    ProfScope ps(gemm_class_name(transa, transb, tri_a, tri_b, nblk * p.nsplit * batch >= 512),
+                 stream, fl, by);
     dim3 g1((unsigned)(nblk * p.nsplit), (unsigned)batch);
     launch_glds<1>(g1, stream, p, tm, tn, transa, transb, tri_a, tri_b);
     VG_LAUNCH_CHECK();
