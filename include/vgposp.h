@@ -513,18 +513,24 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  *     within d steps; tab_nb int [T][m - 1]: row of (offset + offsets[o]) in the table or -1.
  *     T <= 1024, T (m - 1) <= 8192.
  *   vgposp_exact_prepare(flags = 1): round 0 from those bounds (cache = upper bounds).
- *   vgposp_exact_argmax:  the arg-max candidate of the cache -> `cand` (vgposp_exact_buffers).
- *   vgposp_exact_topb:    the B <= 8 best entries of the cache over V \ A, best first (the first is
- *     the arg-max): out int64 [B + 1] (device) = count, candidates.
- *   vgposp_exact_refine:  Q e_c for the nb <= 8 candidates cands[j] (device int64) by one batched
- *     CG into column slots slots[j] (device int, < 2 kmax); each Q_cc becomes exact and the
- *     candidate's cache entry the reference's value (scored with the A of its last re-score).
- *   vgposp_exact_pick:    cand (refined, column in `slot`) becomes pick `round`.
+ *   vgposp_exact_steps_reset: clears the rounds' control block (after prepare, before the rounds).
+ *   vgposp_exact_steps:   rounds [round0, round1), decided on the device.  Each round is one
+ *     kernel that takes the arg-max of the cache over V \ A (lowest index on ties) and either
+ *     picks it (its Q_yy exact, its column in a slot: picks[round] / pick_delta[round], then the
+ *     window update below) or STALLS: the control block records the round and the refinement
+ *     batch (the `batch` <= 8 best entries without a column, each given a free column slot or the
+ *     oldest unpinned one); every later kernel of the issued rounds then does nothing.
+ *   vgposp_exact_refine_pending: Q e_c for the pending batch by one batched CG (columns into
+ *     their slots); each Q_cc becomes exact and the candidate's cache entry the reference's value
+ *     (scored with the A of its last re-score); clears the stall.
+ *   vgposp_exact_ctl:     device address of the control block, int32 [8]: stalled round (-1:
+ *     none), pending batch size, refined-not-picked count, refinement batches, candidates refined.
  *   vgposp_exact_update:  after pick `round`: the factor rows and the window re-score (upper
- *     bounds where Q_yy is still only bounded).
- *   The caller loops top-B -> (refine the batch while the arg-max is not refined) -> pick ->
- *   update: refining the B best entries together (one batched CG, the same launches as one column)
- *   prepares the columns of the next rounds' picks, which are mostly among them.
+ *     bounds where Q_yy is still only bounded); vgposp_exact_steps issues it per round.
+ *   The caller issues rounds, reads the control block, and on a stall refines the pending batch
+ *   and re-issues the rounds from the stalled one: one host read per refinement batch (the B best
+ *   entries are refined together, one batched CG, the launches of one column; the next rounds'
+ *   picks are mostly among them).
  *
  *   vgposp_exact_buffers: device addresses of the column slots [2 kmax][b0 b1 b2] (box-local, C
  *     order, box dims b_d = min(2 radius cg_iters + 1, I_d)), their box origins int64
@@ -545,12 +551,13 @@ int vgposp_exact_coef(VGPOSP_EXACT_ARGS, void* stream);
 int vgposp_exact_bounds(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
                         const int* tab_cnt, int T, int K, double hi_scale, int64_t c0, int64_t c1,
                         void* stream);
-int vgposp_exact_argmax(VGPOSP_EXACT_ARGS, void* stream);
-int vgposp_exact_refine(VGPOSP_EXACT_ARGS, int nb, const int64_t* cands, const int* slots,
-                        const int64_t* picks, double cg_tol, void* stream);
-int vgposp_exact_topb(VGPOSP_EXACT_ARGS, int B, int64_t* out, void* stream);
-int vgposp_exact_pick(VGPOSP_EXACT_ARGS, int round, int slot, int64_t* picks, double* pick_delta,
-                      void* stream);
+int vgposp_exact_steps_reset(VGPOSP_EXACT_ARGS, void* stream);
+int vgposp_exact_steps(VGPOSP_EXACT_ARGS, int round0, int round1, int batch, int64_t* picks,
+                       double* pick_delta, void* stream);
+int vgposp_exact_refine_pending(VGPOSP_EXACT_ARGS, int batch, const int64_t* picks, double cg_tol,
+                                void* stream);
+int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
+                     int cg_iters, int** ctl);
 int vgposp_exact_update(VGPOSP_EXACT_ARGS, int round, const int64_t* picks, void* stream);
 int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
                          int cg_iters, double** qcols, int64_t** boxlo, int** cgstate,

@@ -1,0 +1,45 @@
+"""C4 (128^3, k = 50, beta 4, cutoff 3) end-to-end run time, as bench.py's c4 line measures it:
+python tools/c4_time.py [batch ...] -> one JSON line per refinement batch size: mean ms over 10
+runs, picks vs tests/golden/c4_picks.json, refinements / batches / host reads, and a profiled run's
+per-phase event times."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vgposp_amd import _lib  # noqa: E402
+from vgposp_amd.sparse_placement import ExactTaperPlacement  # noqa: E402
+from vgposp_amd.workloads import c4_grid  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+want = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_picks.json")))["picks"]
+X, shape, ls = c4_grid()
+run = ExactTaperPlacement(X, shape, 50, 3, 4.0, ls=ls, diag_shift=0.01 + 1e-6, method="bounds")
+g = run.greedy
+for B in [int(v) for v in sys.argv[1:]] or [8]:
+    orig = g.run_bounded
+    g.run_bounded = lambda q, k, _o=orig, _b=B: _o(q, k, batch=_b)
+    run.run()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run.run()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    picks = [int(v) for v in g.picks[:50].cpu()]
+    _lib.prof_enable(True)
+    run.run()
+    torch.cuda.synchronize()
+    prof = _lib.prof_dump()
+    _lib.prof_enable(False)
+    g.run_bounded = orig
+    print(json.dumps({"batch": B, "ms_mean": 1e3 * sum(ts) / len(ts), "ms_min": 1e3 * min(ts),
+                      "picks_equal": picks == want, "refinements": g.refinements,
+                      "batches": g.refine_batches, "host_reads": getattr(g, "host_reads", None),
+                      "prof_ms": {k: round(v[0], 3) for k, v in prof.items()},
+                      "prof_launches": {k: v[1] for k, v in prof.items()}}), flush=True)

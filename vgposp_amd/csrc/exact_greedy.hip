@@ -72,10 +72,26 @@ struct ExactWS {
   int* slot_of_round; // [kmax]: the column slot of pick t
   unsigned char* qexact;  // [n]: 1 = qdiag[y] is Q_yy, 0 = an upper bound of it
   unsigned char* lastA;   // [n]: |A| when y's cache entry was last scored (0: round 0)
-  long long* cand;    // [2]: the arg-max candidate of vgposp_exact_argmax
+  long long* cand;    // [2]: scratch (the arg-max candidate of the round-3 host loop)
   double* gersh;      // [2 + 2 CG_BLOCKS]: lambda_min / lambda_max bounds, then partials
+  // device-side rounds (vgposp_exact_steps): the refine-or-pick decision never leaves the GPU
+  int* ctl;           // [CTL_N]: see CTL_* below
+  long long* rl_cand; // [nslots]: the refined candidate held in each column slot (-1: free)
+  int* rl_age;        // [nslots]: refinement order (the oldest unpinned slot is recycled first)
+  unsigned char* rl_pin;  // [nslots]: 1 = the slot is a pick's column (never recycled)
+  long long* rf_cand; // [CG_B]: the pending refinement batch (-1: unused column)
+  int* rf_slot;       // [CG_B]
   size_t bytes;
 };
+
+// ctl[]: the rounds' control block (device memory; the host reads it once per refinement event)
+constexpr int CTL_STALL = 0;     // the round whose arg-max needs a refinement (-1: none)
+constexpr int CTL_NB = 1;        // candidates in the pending batch (rf_cand / rf_slot)
+constexpr int CTL_UNPICKED = 2;  // refined candidates not (yet) picked
+constexpr int CTL_EVENTS = 3;    // refinement batches in this run
+constexpr int CTL_REFINED = 4;   // candidates refined in this run
+constexpr int CTL_AGE = 5;       // refinement counter (rl_age)
+constexpr int CTL_N = 8;
 
 // coefficient rows padded to an even count of doubles (16-byte aligned rows: two-double loads)
 __host__ __device__ constexpr int coef_stride(int m) { return (m + 1) & ~1; }
@@ -127,6 +143,12 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
   w.lastA = (unsigned char*)take((size_t)n);
   w.cand = (long long*)take(16);
   w.gersh = (double*)take(8 * (2 + 2 * (size_t)CG_BLOCKS));
+  w.ctl = (int*)take(4 * CTL_N);
+  w.rl_cand = (long long*)take(8 * (size_t)exact_slots(kmax));
+  w.rl_age = (int*)take(4 * (size_t)exact_slots(kmax));
+  w.rl_pin = (unsigned char*)take((size_t)exact_slots(kmax));
+  w.rf_cand = (long long*)take(8 * CG_B);
+  w.rf_slot = (int*)take(4 * CG_B);
   w.bytes = off;
   return w;
 }
@@ -595,31 +617,6 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_select_kernel(
   if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
 }
 
-// Bounded-lazy path: the arg-max candidate -> cand[0] (nothing else changes).
-__global__ __launch_bounds__(SEL_THREADS) void exact_argmax_kernel(ExactWS w, long long nsb) {
-  const long long a = block_argmax(w, nsb);
-  if (threadIdx.x == 0) w.cand[0] = a;
-}
-
-// Bounded-lazy path: pick cand[0] (refined, its column in `slot`) as pick `round`.
-__global__ __launch_bounds__(64) void exact_pick_kernel(double* cache, unsigned char* sel,
-                                                        long long n, ExactWS w, long long nblk,
-                                                        int round, int slot, long long* picks,
-                                                        double* pick_delta) {
-  const long long a = w.cand[0];
-  if (threadIdx.x == 0) {
-    picks[round] = a;
-    if (pick_delta) pick_delta[round] = a >= 0 ? cache[a] : 0.0;
-    w.slot_of_round[round] = slot;
-    if (a >= 0) {
-      sel[a] = 1;
-      cache[a] = 0.0;
-    }
-  }
-  __syncthreads();
-  if (a >= 0) wave_refresh_keys(cache, sel, w, n, nblk, a);
-}
-
 // Column j of a batched CG solve: its vectors and scalars in the workspace.
 struct CGCol {
   double *r, *p0, *p1, *q, *part_pq, *part_rr, *rr;
@@ -880,14 +877,12 @@ __device__ int block_topb(int cnt, int B, KeyFn key, double* sv, long long* si, 
   return got;
 }
 
-// The B best cache entries over V \ A (vgposp_exact_topb): the B best superblocks contain them,
-// the B best blocks of those contain them, so three small top-B passes in one workgroup find them.
-// out[0] = count, out[1 ..] = the candidates, best first (out[1] is the arg-max).
-__global__ __launch_bounds__(SEL_THREADS) void exact_topb_kernel(const double* cache,
-                                                                 const unsigned char* sel,
-                                                                 long long n, ExactWS w,
-                                                                 long long nblk, long long nsb,
-                                                                 int B, long long* out) {
+// The B best cache entries over V \ A: the B best superblocks contain them, the B best blocks of
+// those contain them, so three small top-B passes in one workgroup find them.  out[0] = count,
+// out[1 ..] = the candidates, best first (out[1] is the arg-max).  The whole workgroup calls it.
+__device__ void block_topb_entries(const double* cache, const unsigned char* sel, long long n,
+                                   const ExactWS& w, long long nblk, long long nsb, int B,
+                                   long long* out) {
   __shared__ double sv[SEL_THREADS / 64];
   __shared__ long long si[SEL_THREADS / 64];
   __shared__ long long tidx[CG_B];
@@ -932,6 +927,107 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_topb_kernel(const double* c
   if (threadIdx.x == 0) {
     out[0] = g3;
     for (int b = 0; b < g3; ++b) out[1 + b] = tidx[b];
+  }
+  __syncthreads();
+}
+
+// Device-side rounds, control block reset (the start of a bounded-lazy run).
+__global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int nslots) {
+  const int t = threadIdx.x;
+  if (t < CTL_N) w.ctl[t] = t == CTL_STALL ? -1 : 0;
+  for (int i = t; i < nslots; i += blockDim.x) {
+    w.rl_cand[i] = -1;
+    w.rl_age[i] = 0;
+    w.rl_pin[i] = 0;
+  }
+  if (t < CG_B) {
+    w.rf_cand[t] = -1;
+    w.rf_slot[t] = 0;
+  }
+}
+
+// One round of the bounded-lazy rounds, decided on the device (vgposp_exact_steps): the arg-max
+// of the cache; if its Q_yy is exact (a refined candidate, its CG column in a slot) it is picked
+// (marked selected, its cache entry 0, its keys refreshed); otherwise the round STALLS: ctl[STALL] = round, and the B best
+// cache entries that have no column yet become the pending refinement batch (rf_cand / rf_slot,
+// ctl[NB]), each given a free slot or the oldest unpinned one — the host loop's rule
+// (sparse_placement.ExactWindowGreedy.run_bounded, round 3).  Every later kernel of the rounds
+// sees the stall (picks[round] stays -1, ctl[STALL] >= 0) and does nothing, until the host has
+// run the refinement (exact_refine_end_kernel clears the stall) and re-issues the rounds from
+// the stalled one.  One workgroup.
+__global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(double* cache, unsigned char* sel,
+                                                                 long long n, ExactWS w,
+                                                                 long long nblk, long long nsb,
+                                                                 int nslots, int round, int B,
+                                                                 long long* picks,
+                                                                 double* pick_delta) {
+  __shared__ int s_slot;
+  __shared__ long long top[CG_B + 1];
+  if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
+  const long long a = block_argmax(w, nsb);
+  if (threadIdx.x == 0) s_slot = -1;
+  __syncthreads();
+  if (a >= 0)
+    for (int i = threadIdx.x; i < nslots; i += SEL_THREADS)
+      if (w.rl_cand[i] == a) s_slot = i;
+  __syncthreads();
+  const int slot = s_slot;
+  if (a < 0 || slot >= 0) {  // pick (no candidate left: picks[round] = -1, nothing changes)
+    if (threadIdx.x == 0) {
+      picks[round] = a;
+      if (pick_delta) pick_delta[round] = a >= 0 ? cache[a] : 0.0;
+      if (a >= 0) {
+        w.slot_of_round[round] = slot;
+        w.rl_pin[slot] = 1;
+        w.ctl[CTL_UNPICKED] -= 1;
+        sel[a] = 1;
+        cache[a] = 0.0;
+      }
+    }
+    __syncthreads();
+    if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
+    return;
+  }
+  // stall: the B best entries without a column become the refinement batch
+  block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
+  if (threadIdx.x == 0) {
+    long long todo[CG_B];
+    int nt = 0;
+    for (int b = 0; b < (int)top[0]; ++b) {
+      const long long y = top[1 + b];
+      bool has = false;
+      for (int i = 0; i < nslots; ++i) has = has || w.rl_cand[i] == y;
+      if (!has) todo[nt++] = y;
+    }
+    if (nt == 0) todo[nt++] = a;
+    int nb = 0;
+    for (int j = 0; j < nt; ++j) {
+      int slot_j = -1;
+      for (int i = 0; i < nslots && slot_j < 0; ++i)
+        if (w.rl_cand[i] < 0) slot_j = i;  // a free slot (lowest first)
+      if (slot_j < 0) {  // recycle the oldest refined candidate not picked and not in the batch
+        int best_age = 0x7fffffff;
+        for (int i = 0; i < nslots; ++i) {
+          if (w.rl_pin[i]) continue;
+          bool in_batch = false;
+          for (int q = 0; q < nt; ++q) in_batch = in_batch || todo[q] == w.rl_cand[i];
+          if (!in_batch && w.rl_age[i] < best_age) {
+            best_age = w.rl_age[i];
+            slot_j = i;
+          }
+        }
+        if (slot_j < 0) break;
+        w.ctl[CTL_UNPICKED] -= 1;  // its candidate loses its column (it is bounded again)
+      }
+      w.rl_cand[slot_j] = todo[j];
+      w.rl_age[slot_j] = w.ctl[CTL_AGE]++;
+      w.rf_cand[nb] = todo[j];
+      w.rf_slot[nb] = slot_j;
+      ++nb;
+    }
+    for (int j = nb; j < CG_B; ++j) w.rf_cand[j] = -1;
+    w.ctl[CTL_NB] = nb;
+    w.ctl[CTL_STALL] = round;
   }
 }
 
@@ -1024,10 +1120,13 @@ __global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* q
                                                               ExactWS w, long long nblk, int nb,
                                                               const int* slots,
                                                               const long long* cands,
-                                                              const long long* picks) {
+                                                              const long long* picks,
+                                                              int resume) {
+  int done = 0;
   for (int j = 0; j < nb; ++j) {
     const long long c = cands[j];
     if (c < 0) continue;
+    ++done;
     const double qcc = qslot_at(w, slots[j], c, a.I1, a.I2);
     const double d = wave_rescore<KIND>(a, w, global_rows(w, a.kmax), picks, (int)w.lastA[c], c,
                                         qcc, true);
@@ -1043,6 +1142,12 @@ __global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* q
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (resume && threadIdx.x == 0) {  // device-side rounds: the stalled round may go on
+    w.ctl[CTL_UNPICKED] += done;
+    w.ctl[CTL_REFINED] += done;
+    w.ctl[CTL_EVENTS] += 1;
+    w.ctl[CTL_STALL] = -1;
   }
 }
 
@@ -1321,11 +1426,12 @@ int exact_round_t(const EArgs& a, const double* qdiag, double* cache, unsigned c
 template <int KIND>
 int exact_refine_t(const EArgs& a, double* qdiag, double* cache, unsigned char* sel,
                    const ExactWS& w, int nb, const long long* cands, const int* slots,
-                   const long long* picks, int radius, int cg_iters, double cg_tol, hipStream_t s) {
+                   const long long* picks, int radius, int cg_iters, double cg_tol, hipStream_t s,
+                   int resume = 0) {
   const long long nblk = ceil_div(a.n, EB);
   if (int rc = exact_cg_run(a, w, nb, slots, cands, radius, cg_iters, cg_tol, s)) return rc;
   hipLaunchKernelGGL(exact_refine_end_kernel<KIND>, dim3(1), dim3(64), 0, s, a, qdiag, cache, sel, w,
-                     nblk, nb, slots, cands, picks);
+                     nblk, nb, slots, cands, picks, resume);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -1435,55 +1541,51 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   return 0;
 }
 
-extern "C" int vgposp_exact_argmax(VGPOSP_EXACT_PARAMS, void* stream) {
-  VGPOSP_EXACT_PROLOGUE("vgposp_exact_argmax");
-  const long long nsb = ceil_div(ceil_div(a.n, EB), ESB);
-  ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
-  hipLaunchKernelGGL(exact_argmax_kernel, dim3(1), dim3(SEL_THREADS), 0, s, w, nsb);
+extern "C" int vgposp_exact_steps_reset(VGPOSP_EXACT_PARAMS, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_steps_reset");
+  (void)a;
+  hipLaunchKernelGGL(exact_steps_reset_kernel, dim3(1), dim3(256), 0, s, w, exact_slots(kmax));
   VG_LAUNCH_CHECK();
   return 0;
 }
 
-extern "C" int vgposp_exact_refine(VGPOSP_EXACT_PARAMS, int nb, const int64_t* cands,
-                                   const int* slots, const int64_t* picks, double cg_tol,
-                                   void* stream) {
-  VGPOSP_EXACT_PROLOGUE("vgposp_exact_refine");
-  VG_CHECK_ARG(nb >= 1 && nb <= CG_B, 24);
-  VG_CHECK_ARG(cands != nullptr, 25);
-  VG_CHECK_ARG(slots != nullptr, 26);
+extern "C" int vgposp_exact_steps(VGPOSP_EXACT_PARAMS, int round0, int round1, int batch,
+                                  int64_t* picks, double* pick_delta, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_steps");
+  VG_CHECK_ARG(round0 >= 0 && round0 <= round1 && round1 <= kmax, 24);
+  VG_CHECK_ARG(batch >= 1 && batch <= CG_B, 26);
   VG_CHECK_ARG(picks != nullptr, 27);
-  VG_CHECK_ARG(cg_tol >= 0.0, 28);
-  const long long* ck = reinterpret_cast<const long long*>(cands);
+  const long long nblk = ceil_div(a.n, EB), nsb = ceil_div(nblk, ESB);
+  long long* pk = reinterpret_cast<long long*>(picks);
+  for (int r = round0; r < round1; ++r) {
+    {
+      ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
+      hipLaunchKernelGGL(exact_step_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
+                         nblk, nsb, exact_slots(kmax), r, batch, pk, pick_delta);
+      VG_LAUNCH_CHECK();
+    }
+    if (r + 1 < kmax) {  // the window of pick r (no-op when the round stalled: picks[r] = -1)
+      const int rc = dispatch_kind(kind, [&](auto K) {
+        return exact_update_t<decltype(K)::value>(a, qdiag, cache, selected, w, r, pk, s);
+      });
+      if (rc) return rc;
+    }
+  }
+  return 0;
+}
+
+extern "C" int vgposp_exact_refine_pending(VGPOSP_EXACT_PARAMS, int batch, const int64_t* picks,
+                                           double cg_tol, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_refine_pending");
+  VG_CHECK_ARG(batch >= 1 && batch <= CG_B, 24);
+  VG_CHECK_ARG(picks != nullptr, 25);
+  VG_CHECK_ARG(cg_tol >= 0.0, 26);
   const long long* pk = reinterpret_cast<const long long*>(picks);
   return dispatch_kind(kind, [&](auto K) {
     return exact_refine_t<decltype(K)::value>(a, const_cast<double*>(qdiag), cache, selected, w,
-                                              nb, ck, slots, pk, radius, cg_iters, cg_tol, s);
+                                              batch, w.rf_cand, w.rf_slot, pk, radius, cg_iters,
+                                              cg_tol, s, 1);
   });
-}
-
-extern "C" int vgposp_exact_topb(VGPOSP_EXACT_PARAMS, int B, int64_t* out, void* stream) {
-  VGPOSP_EXACT_PROLOGUE("vgposp_exact_topb");
-  VG_CHECK_ARG(B >= 1 && B <= CG_B, 24);
-  VG_CHECK_ARG(out != nullptr, 25);
-  const long long nblk = ceil_div(a.n, EB), nsb = ceil_div(nblk, ESB);
-  ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
-  hipLaunchKernelGGL(exact_topb_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
-                     nblk, nsb, B, reinterpret_cast<long long*>(out));
-  VG_LAUNCH_CHECK();
-  return 0;
-}
-
-extern "C" int vgposp_exact_pick(VGPOSP_EXACT_PARAMS, int round, int slot, int64_t* picks,
-                                 double* pick_delta, void* stream) {
-  VGPOSP_EXACT_PROLOGUE("vgposp_exact_pick");
-  VG_CHECK_ARG(round >= 0 && round < kmax, 24);
-  VG_CHECK_ARG(slot >= 0 && slot < exact_slots(kmax), 25);
-  VG_CHECK_ARG(picks != nullptr, 26);
-  const long long nblk = ceil_div(a.n, EB);
-  hipLaunchKernelGGL(exact_pick_kernel, dim3(1), dim3(64), 0, s, cache, selected, a.n, w, nblk,
-                     round, slot, reinterpret_cast<long long*>(picks), pick_delta);
-  VG_LAUNCH_CHECK();
-  return 0;
 }
 
 extern "C" int vgposp_exact_update(VGPOSP_EXACT_PARAMS, int round, const int64_t* picks,
@@ -1510,5 +1612,14 @@ extern "C" int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2
   if (slot_of_round) *slot_of_round = w.slot_of_round;
   if (cand) *cand = reinterpret_cast<int64_t*>(w.cand);
   if (gersh) *gersh = w.gersh;
+  return 0;
+}
+
+extern "C" int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
+                                int radius, int cg_iters, int** ctl) {
+  clear_error();
+  VG_CHECK_ARG(ws != nullptr, 1);
+  VG_CHECK_ARG(ctl != nullptr, 9);
+  *ctl = exact_layout(ws, I0, I1, I2, m, kmax, (int64_t)radius * cg_iters).ctl;
   return 0;
 }

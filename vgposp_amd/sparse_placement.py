@@ -355,12 +355,23 @@ class FrontalSelectedInverse:
                 raise CholeskyError(bad[1], bad[0])
 
 
+_REACH = {}
+
+
 def reach_table(offsets, K):
     """The grid offsets within K stencil steps of a node (breadth-first over the stencil
     ``offsets`` [m-1, 3]), sorted by step count, then C order: (tab [T, 3] int32 with the node
     itself first, cnt [K + 1] int32 = offsets within d steps, nb [T, m-1] int32 = row of
     tab[i] + offsets[o] in the table or -1).  The K-step Krylov space of e_y lives on exactly these
-    nodes (around y, clipped to the grid)."""
+    nodes (around y, clipped to the grid).  Depends on the stencil only (not on the data), so it
+    is built once per (stencil, K)."""
+    key = (np.asarray(offsets, dtype=np.int64).tobytes(), int(K))
+    if key not in _REACH:
+        _REACH[key] = _reach_table(offsets, K)
+    return _REACH[key]
+
+
+def _reach_table(offsets, K):
     offs = [tuple(int(v) for v in o) for o in np.asarray(offsets, dtype=np.int64).reshape(-1, 3)]
     dist = {(0, 0, 0): 0}
     frontier = [(0, 0, 0)]
@@ -517,9 +528,16 @@ class ExactWindowGreedy:
         reference's cached deltas; an arg-max that lands on a candidate whose Q_yy is only bounded
         refines it (its CG column; its cache entry becomes the reference's value) and the arg-max
         is taken again, so every pick is the reference's arg-max.  The refinement takes the
-        ``batch`` (<= 8) best entries together — one batched CG costs the launches of one column,
-        and the next rounds' picks are mostly among them.  One host read per arg-max (and one per
-        top-B when a refinement is due)."""
+        ``batch`` (<= 8) best entries without a column together — one batched CG costs the
+        launches of one column, and the next rounds' picks are mostly among them.
+
+        The refine-or-pick decision is made ON THE DEVICE (vgposp_exact_steps: one kernel per
+        round takes the arg-max and either picks it or stalls the rounds and writes the
+        refinement batch).  The host reads the 32-byte control block once per refinement event
+        (about 7 per 128^3 run), refines the pending batch (vgposp_exact_refine_pending) and
+        re-issues the rounds from the stalled one — as many as there are refined candidates not
+        yet picked, plus the one that will stall next.  Round 3 read the device twice per
+        arg-max instead (57 host reads per run)."""
         if k > self.kmax:
             raise ValueError(f"k = {k} > kmax = {self.kmax}")
         B = REFINE_BATCH if batch is None else int(batch)
@@ -527,54 +545,36 @@ class ExactWindowGreedy:
             raise ValueError(f"batch must be in [1, 8], got {B}")
         self.picks.fill_(-1)
         args = self._args(qdiag)
-        call("vgposp_exact_prepare", *args, 1, _stream())
-        dev = self.p.device
-        top = torch.empty(9, dtype=torch.int64, device=dev)
-        cands = torch.empty(8, dtype=torch.int64, device=dev)
-        slots = torch.empty(8, dtype=torch.int32, device=dev)
-        colslot, order, free = {}, [], list(range(self.nslots - 1, -1, -1))
-        self.refinements = self.refine_batches = 0
-        cand = self.ws[self._buffers()[4]:][:8].view(torch.int64)
-        for t in range(k):
-            while True:
-                call("vgposp_exact_argmax", *args, _stream())
-                c = int(cand.item())
-                if c < 0 or c in colslot:
-                    break
-                # the arg-max needs its column: refine the B best entries together
-                call("vgposp_exact_topb", *args, B, _p(top), _stream())
-                got = top.cpu().tolist()
-                todo = [y for y in got[1:1 + got[0]] if y not in colslot] or [c]
-                todo_set = set(todo)
-                use = []
-                for y in todo:
-                    if free:
-                        slot = free.pop()
-                    else:  # recycle the oldest refined candidate that is not picked or in the batch
-                        old = next((o for o in order if o not in todo_set), None)
-                        if old is None:
-                            break
-                        order.remove(old)
-                        slot = colslot.pop(old)
-                    use.append((y, slot))
-                cands[:len(use)].copy_(torch.tensor([y for y, _ in use], dtype=torch.int64))
-                slots[:len(use)].copy_(torch.tensor([s for _, s in use], dtype=torch.int32))
-                call("vgposp_exact_refine", *args, len(use), _p(cands), _p(slots), _p(self.picks),
-                     self.cg_tol, _stream())
-                for y, slot in use:
-                    colslot[y] = slot
-                    order.append(y)
-                self.refinements += len(use)
-                self.refine_batches += 1
-            if c < 0:
+        st = _stream()
+        call("vgposp_exact_prepare", *args, 1, st)
+        call("vgposp_exact_steps_reset", *args, st)
+        ctl = self._ctl()
+        pk, pd = _p(self.picks), _p(self.pick_delta)
+        call("vgposp_exact_steps", *args, 0, 1, B, pk, pd, st)  # round 0 stalls: nothing refined
+        issued, reads = 1, 0
+        while True:
+            c = ctl.cpu().tolist()  # stall round, batch size, refined-unpicked, events, refined
+            reads += 1
+            stall = c[0]
+            if stall >= 0:
+                call("vgposp_exact_refine_pending", *args, B, pk, self.cg_tol, st)
+                r0, r1 = stall, min(k, stall + c[2] + c[1] + 1)
+            elif issued < k:
+                r0, r1 = issued, min(k, issued + max(c[2], 0) + 1)
+            else:
                 break
-            slot = colslot[c]
-            order.remove(c)      # pinned: the pick's column is a row of Q_A
-            call("vgposp_exact_pick", *args, t, slot, _p(self.picks), _p(self.pick_delta),
-                 _stream())
-            if t < k - 1:
-                call("vgposp_exact_update", *args, t, _p(self.picks), _stream())
+            call("vgposp_exact_steps", *args, r0, r1, B, pk, pd, st)
+            issued = r1
+        self.refinements, self.refine_batches, self.host_reads = c[4], c[3], reads
         return self.picks[:k]
+
+    def _ctl(self):
+        """The device control block of the rounds (int32 [8], vgposp_exact_buffers)."""
+        p = ctypes.c_void_p()
+        call("vgposp_exact_ctl", _p(self.ws), *self.p.shape, self.p.m, self.kmax, self.radius,
+             self.cg_iters, ctypes.byref(p))
+        off = p.value - self.ws.data_ptr()
+        return self.ws[off: off + 32].view(torch.int32)
 
     def _buffers(self):
         ptrs = [ctypes.c_void_p() for _ in range(6)]
