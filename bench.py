@@ -64,7 +64,9 @@ def parse():
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                         "the multi-rank path on one GPU with VGPOSP_BENCH_DEVICE=0)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r3.json"),
+    p.add_argument("--c4-pmc", default=os.path.join(ROOT, "profiles", "pmc_c4_r4.json"),
+                   help="per-run C4 kernel bytes from rocprofv3 PMC passes (tools/pmc_c4.py)")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r4.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
 
@@ -142,6 +144,10 @@ def cpu_baseline(args, N):
     op.placement_algorithm_2(Sp, args.cpu_k, trace=trace)
     t_pinv = time.perf_counter() - t0
     nevals = sum(1 for e in trace if e[0] != "select")
+    # the GPU on the SAME samples (so the two can be read side by side)
+    gpu_same = gpu_on_sample(S_keep := sigma(shape), args.k)
+    gpu_ref = gpu_on_sample(Sp, args.cpu_k)
+    del S_keep
     nc = 6144
     Sc = sigma((24, 16, 16))
     t0 = time.perf_counter()
@@ -160,15 +166,43 @@ def cpu_baseline(args, N):
                    f"jittered {shape[0]}x{shape[1]}x{shape[2]} grid (N={n_inc}), k={args.k}: "
                    f"{t_inc:.1f} s; the GPU line is at N={N}, where the O(N^3) init alone is "
                    f"{(N / n_inc) ** 3:.0f}x this sample's"),
+        "gpu_same_sample": gpu_same,
         "reference_algorithm": {
             "value": args.cpu_k / t_pinv, "unit": "placements/s",
             "sample": (f"pinv restatement of placement_algorithm2.placement_algorithm_2 on a "
                        f"jittered {ps[0]}x{ps[1]}x{ps[2]} grid (N={len(Sp)}), k={args.cpu_k}: "
-                       f"{nevals} delta evaluations (one SVD each) in {t_pinv:.1f} s")},
+                       f"{nevals} delta evaluations (one SVD each) in {t_pinv:.1f} s"),
+            "gpu_same_sample": gpu_ref},
         "cholesky_gflops": nc ** 3 / 3 / tc / 1e9,
         "cholesky_sample": f"numpy.linalg.cholesky at N={nc}",
         "cpu_model": cpu_model(),
     }
+
+
+def gpu_on_sample(S, k, reps=5):
+    """placements/s of the HIP path on the host covariance S (device-resident before timing:
+    Sigma copied in, factored in place, k lazy rounds; best of `reps`), with its picks."""
+    import torch
+
+    from vgposp_amd.placement_algorithm2 import GreedyPlacement
+    Sd = torch.as_tensor(S, device="cuda")
+    work = torch.empty_like(Sd)
+    g = GreedyPlacement(work, k)
+    best = None
+    for _ in range(reps + 1):
+        work.copy_(Sd)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.run(k)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    g.check()
+    picks = [int(v) for v in g.selected[:k].cpu()]
+    del g, work, Sd
+    torch.cuda.empty_cache()
+    return {"value": k / best, "unit": "placements/s", "N": int(S.shape[0]), "k": k,
+            "picks_head": picks[:6]}
 
 
 def load_traffic(path, kernel, N, shape, k):
@@ -393,7 +427,8 @@ def c4_line(args, world, rank, barrier, maxtime):
            "exchanged_gb_per_step": (8.0 * (-(-run.prob.n // world)) * (world - 1) / 1e9
                                      if world > 1 else 0.0),
            "rounds_ms": rounds_ms, "refinements": g.refinements,
-           "refine_batches": g.refine_batches,
+           "refine_batches": g.refine_batches, "host_reads": getattr(g, "host_reads", None),
+           "roofline": c4_roofline(run, prof, nb, args.c4_pmc),
            "cg_iterations_per_column": g.cg_iters,
            "breakdown_ms": {n: v[0] for n, v in prof.items()}}
     # the selected-inverse form once: the same picks, and the fp64-MFMA rate of its fronts
@@ -443,16 +478,86 @@ def c4_line(args, world, rank, barrier, maxtime):
     # its picks are the "bit-exact vs CPU" check at full size, its time the C4 CPU baseline
     if world == 1 and rank == 0 and not args.no_cpu:
         from oracle import c4_exact as oc4
-        st = {}
-        cp, _ = oc4.exact_alg3(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6,
-                               stats=st)
+        # at the runtime's default team (OMP_NUM_THREADS: 16 on the GPU box) and at every
+        # logical CPU of the host; the value is the faster of the two
+        runs = {}
+        for th in sorted({oc4.lib().c4o_threads(), os.cpu_count() or 1}):
+            st = {}
+            cp, _ = oc4.exact_alg3(X, shape, k, cutoff, beta, ls=ls, diag_shift=args.noise + 1e-6,
+                                   stats=st, threads=th)
+            runs[th] = (st["seconds"], [int(v) for v in cp] == picks, st["refinements"])
+        best = min(runs, key=lambda t: runs[t][0])
         out["cpu_baseline"] = {
-            "value": k / st["seconds"], "unit": "placements/s", "cores": st["threads"],
-            "kind": "port", "sample": f"the whole workload (128^3, k={k}), one run",
-            "picks_equal": [int(v) for v in cp] == picks, "seconds": st["seconds"],
-            "refinements": st["refinements"],
+            "value": k / runs[best][0], "unit": "placements/s", "cores": best,
+            "os_cpu_count": os.cpu_count(),
+            "by_threads": {str(t): k / v[0] for t, v in runs.items()},
+            "kind": "port", "sample": f"the whole workload (128^3, k={k}), one run per team size",
+            "picks_equal": all(v[1] for v in runs.values()), "seconds": runs[best][0],
+            "refinements": runs[best][2],
             "note": "oracle/c4_exact.c: the same bounded-lazy algorithm 3 in C (OpenMP bounds, "
                     "sequential rounds)"}
+    return out
+
+
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: aggregate L2 bandwidth (4 MiB per XCD, 8 XCDs)
+
+
+def c4_roofline(run, prof, ncand, pmc_path=None):
+    """Rooflines of config C4's two dominant phases from one profiled run (`prof`: prof_fold'ed
+    vgposp_prof_dump), with their algorithmic bytes:
+      exact_bounds: each candidate y reads the coefficient rows of the nodes within K stencil
+        steps (T rows of m doubles: its K-step Krylov space) and writes qdiag[y].  Unique bytes
+        (the coefficient table once + qdiag) against HBM; the per-candidate operand bytes
+        (T m 8 + 8) against the L2, where the neighbouring candidates' shared rows are served.
+      exact_cg: per column and iteration the active cube of (it + 1) stencil radii around the
+        column's centre, 8 (m + 9) bytes per node (coefficient row, r / p / q / x reads and writes).
+    `traffic`: FETCH + WRITE bytes per run from a rocprofv3 PMC pass (profiles/pmc_c4_*.json) when
+    it was measured on this build's sources."""
+    from vgposp_amd._lib import source_hash
+    from vgposp_amd.sparse_placement import reach_table
+    g = run.greedy
+    pr = run.prob
+    m = pr.m
+    K = g.bound[0] if g.bound else None
+    T = len(reach_table(pr.offs_np, K)[0]) if K else 0
+    stride = (m + 1) & ~1
+    b_ms = prof.get("exact_bounds", (0.0,))[0]
+    uniq = pr.n * 8.0 * stride + ncand * 8.0
+    oper = ncand * (8.0 * T * m + 8.0)
+    out = {"kernel": "exact_bounds", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "achieved": uniq / (b_ms * 1e-3) / 1e9 if b_ms else None, "traffic": None,
+           "algorithmic_bytes": uniq, "candidates": ncand, "K": K, "reach_nodes": T,
+           "l2_operand_bytes": oper,
+           "l2_achieved": oper / (b_ms * 1e-3) / 1e9 if b_ms else None, "l2_peak": L2_PEAK_GBS}
+    if out["achieved"]:
+        out["frac"] = out["achieved"] / HBM_PEAK_GBS
+        out["l2_frac"] = out["l2_achieved"] / L2_PEAK_GBS
+    cg_ms = prof.get("exact_cg", (0.0,))[0]
+    box = 2 * g.radius * g.cg_iters + 1
+    node_its = sum(min(2 * (it + 1) * g.radius + 1, box) ** 3 for it in range(g.cg_iters))
+    cg_bytes = g.refinements * node_its * 8.0 * (m + 9)
+    out["cg"] = {"kernel": "exact_cg_a/b", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                 "columns": g.refinements, "iterations": g.cg_iters, "batches": g.refine_batches,
+                 "node_iterations_per_column": node_its, "algorithmic_bytes": cg_bytes,
+                 "achieved": cg_bytes / (cg_ms * 1e-3) / 1e9 if cg_ms else None,
+                 "launch_bound_floor_ms": g.refine_batches * (2 * g.cg_iters + 2) * 6.5e-3}
+    if out["cg"]["achieved"]:
+        out["cg"]["frac"] = out["cg"]["achieved"] / HBM_PEAK_GBS
+    if pmc_path and os.path.exists(pmc_path):
+        t = json.load(open(pmc_path))
+        if t.get("source_sha256") == source_hash("exact") and t.get("workload", {}).get("N") == pr.n:
+            kb = t["kernels"]
+            bnd = [v for kk, v in kb.items() if kk.startswith("exact_bounds")]
+            if bnd:
+                out["traffic"] = sum(v["fetch_bytes_per_run"] + v["write_bytes_per_run"] for v in bnd)
+                out["l2_hit_rate"] = bnd[0].get("l2_hit_rate")
+            cgk = [v for kk, v in kb.items() if kk.startswith("exact_cg")]
+            if cgk:
+                out["cg"]["traffic"] = sum(v["fetch_bytes_per_run"] + v["write_bytes_per_run"]
+                                           for v in cgk)
+            out["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+        else:
+            out["traffic_note"] = "null: the PMC file was measured on other kernel sources"
     return out
 
 
@@ -535,9 +640,25 @@ def grid_sweep(args, world, rank, barrier, maxtime):
         torch.cuda.synchronize()
         barrier()
         dt = maxtime(time.perf_counter() - t0) / 5
-        out[f"{n}^3_tapered_alg3"] = {"N": n ** 3, "placements_per_s": k / dt,
-                                      "ms_per_problem": dt * 1e3,
-                                      "picks_head": [int(v) for v in run.greedy.picks[:6].cpu()]}
+        _lib.prof_enable(True)
+        run.run()
+        torch.cuda.synchronize()
+        sprof = _lib.prof_fold(_lib.prof_dump())
+        _lib.prof_enable(False)
+        picks = [int(v) for v in run.greedy.picks[:k].cpu()]
+        ent = {"N": n ** 3, "placements_per_s": k / dt, "ms_per_problem": dt * 1e3,
+               "picks_head": picks[:6],
+               "roofline": c4_roofline(run, sprof, run.prob.n // world, None)}
+        if world == 1 and rank == 0 and not args.no_cpu:
+            from oracle import c4_exact as oc4
+            st = {}
+            th = os.cpu_count() or 1
+            cp, _ = oc4.exact_alg3(Xc, shp, k, 3, 4.0, ls=lsc, diag_shift=args.noise + 1e-6,
+                                   stats=st, threads=th)
+            ent["cpu_baseline"] = {"value": k / st["seconds"], "unit": "placements/s",
+                                   "cores": th, "kind": "port", "sample": "the whole problem",
+                                   "picks_equal": [int(v) for v in cp] == picks}
+        out[f"{n}^3_tapered_alg3"] = ent
         del run
         torch.cuda.empty_cache()
     out["note"] = ("k = 50 each; 32^3: jittered grid, EQ ls 2h, noise 1e-2 + 1e-6 (the headline's "

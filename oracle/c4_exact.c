@@ -24,6 +24,11 @@
 
 // OpenMP threads the bounds loop runs on.
 int c4o_threads(void) { return omp_get_max_threads(); }
+// the OpenMP team size of the next runs (the CPU baseline times it at OMP_NUM_THREADS and at
+// every CPU of the host)
+void c4o_set_threads(int n) {
+  if (n > 0) omp_set_num_threads(n);
+}
 
 typedef struct {
   const double* X;

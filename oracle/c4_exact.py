@@ -44,6 +44,8 @@ def lib():
                               I32, F, I32, F, I32, I32, P, P, P]
         L.c4o_run.restype = I32
         L.c4o_threads.restype = I32
+        L.c4o_set_threads.argtypes = [I32]
+        L.c4o_set_threads.restype = None
         _lib = L
     return _lib
 
@@ -98,10 +100,12 @@ def cg_iterations(lam_min, lam_max, tol):
 
 
 def exact_alg3(X, shape, k, cutoff, beta=4.0, kind="eq", amp=1.0, ls=1.0, diag_shift=0.0,
-               jitter=TF_JITTER, threshold=TF_SMALL, cg_tol=1e-16, K=None, stats=None):
+               jitter=TF_JITTER, threshold=TF_SMALL, cg_tol=1e-16, K=None, stats=None,
+               threads=None):
     """Algorithm 3 on the tapered covariance of the grid points X (C order) -> (picks [k] int64,
     pick deltas [k]).  ``K`` overrides the bracket's CG steps (any K gives the same picks);
-    ``stats`` (dict) receives refinements, K, cg_iters, the Gershgorin bounds and seconds."""
+    ``stats`` (dict) receives refinements, K, cg_iters, the Gershgorin bounds and seconds;
+    ``threads``: the OpenMP team size (default: OMP_NUM_THREADS / the runtime's)."""
     I0, I1, I2 = (int(s) for s in shape)
     n = I0 * I1 * I2
     X = np.ascontiguousarray(X, dtype=np.float64).reshape(n, 3)
@@ -110,6 +114,8 @@ def exact_alg3(X, shape, k, cutoff, beta=4.0, kind="eq", amp=1.0, ls=1.0, diag_s
     tau = np.ascontiguousarray(tau, dtype=np.float64)
     m1 = len(offs)
     L = lib()
+    if threads:
+        L.c4o_set_threads(int(threads))
     t0 = time.perf_counter()
     coef = np.empty((n, m1 + 1))
     lam = np.zeros(2)

@@ -1,6 +1,6 @@
 """C4 (128^3, k = 50, beta 4, cutoff 3) end-to-end run time, as bench.py's c4 line measures it:
-python tools/c4_time.py [batch ...] -> one JSON line per refinement batch size: mean ms over 10
-runs, picks vs tests/golden/c4_picks.json, refinements / batches / host reads, and a profiled run's
+python tools/c4_time.py [--reps R] [batch ...] -> one JSON line per refinement batch size: mean ms
+over R (10) runs, picks vs tests/golden/c4_picks.json, refinements / batches / host reads, and a profiled run's
 per-phase event times."""
 import json
 import os
@@ -16,16 +16,20 @@ from vgposp_amd.workloads import c4_grid  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 want = json.load(open(os.path.join(ROOT, "tests", "golden", "c4_picks.json")))["picks"]
+args = sys.argv[1:]
+REPS = 10
+if args[:1] == ["--reps"]:
+    REPS, args = int(args[1]), args[2:]
 X, shape, ls = c4_grid()
 run = ExactTaperPlacement(X, shape, 50, 3, 4.0, ls=ls, diag_shift=0.01 + 1e-6, method="bounds")
 g = run.greedy
-for B in [int(v) for v in sys.argv[1:]] or [8]:
+for B in [int(v) for v in args] or [8]:
     orig = g.run_bounded
     g.run_bounded = lambda q, k, _o=orig, _b=B: _o(q, k, batch=_b)
     run.run()
     torch.cuda.synchronize()
     ts = []
-    for _ in range(10):
+    for _ in range(REPS):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run.run()

@@ -269,6 +269,7 @@ KERNEL_SOURCES = {
     "greedy_trmv": ["greedy.hip", "common.h", "Makefile"],
     "greedy_colsq": ["greedy.hip", "common.h", "Makefile"],
     "kernel_matrix": ["kernel_matrix.hip", "psd.h", "common.h", "Makefile"],
+    "exact": ["exact_greedy.hip", "psd.h", "common.h", "Makefile"],
 }
 
 

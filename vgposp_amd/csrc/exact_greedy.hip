@@ -668,6 +668,7 @@ __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long lon
     cc.state[0] = c >= 0 ? 0 : 1;
     cc.state[1] = 0;
   }
+  if (c < 0) return;  // an unused column of the batch: its slot (if any) belongs to someone else
   for (long long l = (long long)blockIdx.x * 256 + threadIdx.x; l < bv;
        l += (long long)gridDim.x * 256) {
     cc.r[l] = l == lc ? 1.0 : 0.0;
@@ -942,7 +943,7 @@ __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int n
   }
   if (t < CG_B) {
     w.rf_cand[t] = -1;
-    w.rf_slot[t] = 0;
+    w.rf_slot[t] = -1;
   }
 }
 
@@ -1025,7 +1026,10 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(double* cache, 
       w.rf_slot[nb] = slot_j;
       ++nb;
     }
-    for (int j = nb; j < CG_B; ++j) w.rf_cand[j] = -1;
+    for (int j = nb; j < CG_B; ++j) {
+      w.rf_cand[j] = -1;
+      w.rf_slot[j] = -1;
+    }
     w.ctl[CTL_NB] = nb;
     w.ctl[CTL_STALL] = round;
   }

@@ -124,14 +124,17 @@ class VGPTrainOp:
     (the reference's training graph, variational_Gaussian_process_example.py:51-102).  Trainables:
     the kernel's softplus amplitude / length_scale, the softplus observation noise variance and
     the inducing_index_points Variable, re-bound into one flat device buffer updated by the HIP
-    Adam kernel.  ``run(feed)`` returns the pre-update loss (device scalar).
+    Adam kernel.  ``run(feed)`` returns the pre-update loss (device scalar).  Call ``check()``
+    after the last ``run`` of a training loop: a replayed step's factorization statuses are read
+    behind the next step, so the last step's are checked only there.
 
     From the second run on, the whole step (posterior, ELBO, reverse pass, Adam: ~400 launches)
     is captured once into a HIP graph and replayed, with the feeds copied into static buffers —
     the same fixed graph a TF1 session runs.  A replayed step's Cholesky statuses are checked
     when the next step has been issued (or by ``check()``), so a non-PD factorization raises
-    CholeskyError one ``run`` late.  Eager when ``graph=False``, for a data-parallel ``group``,
-    or while the library's event timing is on.
+    CholeskyError one ``run`` late.  With a data-parallel ``group`` the step is captured as
+    three graph segments replayed around its two all-reduces.  Eager when ``graph=False`` or
+    while the library's event timing is on.
 
     Scheduling switches (each measured, defaults = the faster setting): ``streams`` the VGP
     step's side-stream bitmask (``VGPObjective``), ``fused_params`` the softplus values in one
@@ -188,7 +191,8 @@ class VGPTrainOp:
                                       trace_adjoint=vgp.trace_adjoint, group=group,
                                       precision=precision, streams=streams, grouped=grouped)
         self.fused = bool(fused_params)
-        self.graph = bool(graph) and group is None
+        # data parallel: the step is captured as graph segments between its two all-reduces
+        self.graph = bool(graph)
         self._runs = 0
         self._g = None  # (graph, feed shapes, static X, static y, loss, statuses)
         self._hstat = None    # two pinned host buffers for the replayed steps' statuses
@@ -234,20 +238,56 @@ class VGPTrainOp:
              (ctypes.c_void_p * 4)(*[g.data_ptr() for _, g in chain]), linalg._stream())
         return loss
 
+    def _capture(self, sX, sy):
+        """Capture the step into HIP graph segments: ONE graph on a single GPU; with a
+        data-parallel group a new segment starts at each of the step's two all-reduces (the
+        [P0, c] partials, the Kzx VJP's), which run between the segment replays — RCCL on the
+        current stream without a host synchronisation, gloo through the host.  The segments share
+        one memory pool and are replayed in capture order.  -> (segments [(graph, tensor to
+        all-reduce after it or None)], loss, status)."""
+        obj = self.objective
+        pool = torch.cuda.graph_pool_handle()
+        segs, infos = [], []
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        cur = [torch.cuda.CUDAGraph()]
+
+        def boundary(t):
+            obj.join_side_streams()
+            cur[0].capture_end()
+            segs.append((cur[0], t))
+            cur[0] = torch.cuda.CUDAGraph()
+            cur[0].capture_begin(pool=pool)
+            return t
+
+        with torch.cuda.stream(cap):
+            cur[0].capture_begin(pool=pool)
+            obj._capture_hook = boundary if obj.group is not None else None
+            try:
+                loss = self._step(sX, sy, infos)
+                status = torch.cat(infos)
+                obj.join_side_streams()
+            finally:
+                obj._capture_hook = None
+            cur[0].capture_end()
+            segs.append((cur[0], None))
+        torch.cuda.current_stream().wait_stream(cap)
+        return segs, loss, status
+
     def _replay(self, Xb, yb):
         key = (tuple(Xb.shape), tuple(yb.shape))
         if self._g is None or self._g[1] != key:
             sX, sy = Xb.clone(), yb.clone()
-            g = torch.cuda.CUDAGraph()
-            infos = []
-            with torch.cuda.graph(g):
-                loss = self._step(sX, sy, infos)
-                status = torch.cat(infos)
-            self._g = (g, key, sX, sy, loss, status)
-        g, _, sX, sy, loss, status = self._g
+            segs, loss, status = self._capture(sX, sy)
+            self._g = (segs, key, sX, sy, loss, status)
+        segs, _, sX, sy, loss, status = self._g
         sX.copy_(Xb)
         sy.copy_(yb)
-        g.replay()
+        for g, t in segs:
+            g.replay()
+            if t is not None:
+                self.objective.allreduce_now(t)
         out = loss.clone()
         # The step's Cholesky statuses go to pinned host memory behind the replay and are checked
         # when the NEXT step has been issued (or by check()): waiting then costs nothing, the GPU

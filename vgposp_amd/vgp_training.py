@@ -154,15 +154,30 @@ class VGPObjective:
         self._Kzx = None
         self._side = None
         self._tail = None  # side stream of the step (Kzb, the vector chain, VJPs, reductions)
+        self._capture_hook = None  # set by VGPTrainOp while capturing a data-parallel step
         self._streams = (7 if self.mixed else 0) if streams is None else int(streams)
         if not 0 <= self._streams <= 7:
             raise ValueError(f"streams must be a bitmask in [0, 7], got {streams!r}")
         self.grouped = bool(grouped)
 
     def _allreduce(self, t):
-        """Sum over the data-parallel group (host-staged for gloo, in place on device for RCCL)."""
+        """Sum over the data-parallel group (host-staged for gloo, in place on device for RCCL).
+        While a segmented HIP graph of the step is being captured (VGPTrainOp with a group), the
+        all-reduce is a segment boundary instead: the capture hook ends the current graph there
+        and the replay runs the all-reduce between the segments."""
         if self.group is None:
             return t
+        if self._capture_hook is not None:
+            return self._capture_hook(t)
+        return self.allreduce_now(t)
+
+    def join_side_streams(self):
+        """The current stream waits for every side stream of the step (a segment boundary)."""
+        cur = torch.cuda.current_stream()
+        for st in (self._side or []) + ([self._tail] if self._tail is not None else []):
+            _wait(cur, st)
+
+    def allreduce_now(self, t):
         dist = torch.distributed
         if dist.get_backend(self.group) == "gloo" and t.device.type != "cpu":
             h = t.cpu()
