@@ -514,12 +514,15 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  *     T <= 1024, T (m - 1) <= 8192.
  *   vgposp_exact_prepare(flags = 1): round 0 from those bounds (cache = upper bounds).
  *   vgposp_exact_steps_reset: clears the rounds' control block (after prepare, before the rounds).
- *   vgposp_exact_steps:   rounds [round0, round1), decided on the device.  Each round is one
- *     kernel that takes the arg-max of the cache over V \ A (lowest index on ties) and either
- *     picks it (its Q_yy exact, its column in a slot: picks[round] / pick_delta[round], then the
- *     window update below) or STALLS: the control block records the round and the refinement
- *     batch (the `batch` <= 8 best entries without a column, each given a free column slot or the
- *     oldest unpinned one); every later kernel of the issued rounds then does nothing.
+ *   vgposp_exact_steps:   rounds [round0, round1) of a run of k picks, decided on the device.
+ *     Each round is two kernels: the first refreshes the arg-max keys of the previous round's
+ *     window, takes the arg-max of the cache over V \ A (lowest index on ties) and either picks
+ *     it (its Q_yy exact, its column in a slot: picks[round] / pick_delta[round], the pick's rows
+ *     of chol(Q_AA) and chol(Sigma_AA + jitter I)) or STALLS: the control block records the round
+ *     and the refinement
+ *     batch (the `batch` <= 32 best entries without a column, each given a free column slot or the
+ *     oldest unpinned one); every later kernel of the issued rounds then does nothing.  The second
+ *     re-scores the window of the pick (upper bounds where Q_yy is still only bounded).
  *   vgposp_exact_refine_pending: Q e_c for the pending batch by one batched CG (columns into
  *     their slots); each Q_cc becomes exact and the candidate's cache entry the reference's value
  *     (scored with the A of its last re-score); clears the stall.
@@ -552,8 +555,8 @@ int vgposp_exact_bounds(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb
                         const int* tab_cnt, int T, int K, double hi_scale, int64_t c0, int64_t c1,
                         void* stream);
 int vgposp_exact_steps_reset(VGPOSP_EXACT_ARGS, void* stream);
-int vgposp_exact_steps(VGPOSP_EXACT_ARGS, int round0, int round1, int batch, int64_t* picks,
-                       double* pick_delta, void* stream);
+int vgposp_exact_steps(VGPOSP_EXACT_ARGS, int round0, int round1, int k, int batch,
+                       int64_t* picks, double* pick_delta, void* stream);
 int vgposp_exact_refine_pending(VGPOSP_EXACT_ARGS, int batch, const int64_t* picks, double cg_tol,
                                 void* stream);
 int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,

@@ -100,7 +100,7 @@ __host__ __device__ constexpr int coef_stride(int m) { return (m + 1) & ~1; }
 __host__ __device__ __forceinline__ int exact_slots(int kmax) { return 2 * kmax; }
 
 constexpr int CG_MAXIT = 512;
-constexpr int CG_B = 8;       // columns solved together by one batched CG (blockIdx.y)
+constexpr int CG_B = 32;      // columns solved together by one batched CG (blockIdx.y)
 
 static size_t ealign(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -731,11 +731,71 @@ __device__ __forceinline__ ActiveCube active_cube(const ExactWS& w, long long I1
   return q;
 }
 
+// 7-point stencil (the reference's beta = 4 taper): after `it` iterations the Krylov vectors of
+// e_c are supported on the Manhattan ball |d0| + |d1| + |d2| <= it around c, an octahedron of
+// about (4/3) R^3 nodes against the (2R + 1)^3 of the bounding cube (6x fewer at R = 29).  Its
+// nodes are walked row by row: the (d0, d1) rows with |d0| + |d1| <= R (2R^2 + 2R + 1 of them),
+// each a contiguous d2 run of 2 (R - |d0| - |d1|) + 1 nodes, one wave per row.
+__device__ __forceinline__ long long diamond_rows(long long R) { return 2 * R * R + 2 * R + 1; }
+
+// Row `rw` (< diamond_rows(R)) of the diamond, rows ordered by s = |d0| + |d1| (shell s >= 1 has
+// 4 s rows) -> (d0, d1).
+__device__ __forceinline__ void diamond_row(long long rw, long long& d0, long long& d1) {
+  if (rw == 0) {
+    d0 = d1 = 0;
+    return;
+  }
+  // shell s: rows [2 s^2 - 2 s + 1, 2 s^2 + 2 s + 1)
+  long long s = (long long)((sqrt(2.0 * (double)rw - 1.0) + 1.0) * 0.5);
+  while (2 * s * s - 2 * s + 1 > rw) --s;
+  while (2 * (s + 1) * (s + 1) - 2 * (s + 1) + 1 <= rw) ++s;
+  const long long e = rw - (2 * s * s - 2 * s + 1);  // 0 .. 4 s - 1 around the diamond
+  const long long side = e / s, k = e % s;
+  switch (side) {
+    case 0: d0 = s - k; d1 = k; break;        // ( s, 0) -> (0,  s)
+    case 1: d0 = -k; d1 = s - k; break;       // ( 0, s) -> (-s, 0)
+    case 2: d0 = -s + k; d1 = -k; break;      // (-s, 0) -> (0, -s)
+    default: d0 = k; d1 = -s + k; break;      // ( 0,-s) -> ( s, 0)
+  }
+}
+
+// Visit the active nodes of iteration `it` (grid coordinates): the active cube, thread t its
+// t-th node; or (OCT) the Manhattan ball of radius it + 1 around the centre a, one wave per
+// diamond row, lane l the row's l-th node (rows longer than 64 nodes: l, l + 64, ...).
+template <bool OCT, class F>
+__device__ __forceinline__ void cg_walk(const ExactWS& w, const ActiveCube& q, long long I0,
+                                        long long I1, long long I2, long long a, int it, F&& f) {
+  if (!OCT) {
+    for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
+         t += (long long)gridDim.x * CG_T) {
+      const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
+                      g2 = q.c2 + t % q.e2;
+      f(g0, g1, g2);
+    }
+    return;
+  }
+  const long long R = min((long long)it + 1, w.H);
+  const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
+  const int lane = threadIdx.x & 63;
+  const long long nrows = diamond_rows(R);
+  for (long long rw = (long long)blockIdx.x * (CG_T / 64) + (threadIdx.x >> 6); rw < nrows;
+       rw += (long long)gridDim.x * (CG_T / 64)) {
+    long long d0, d1;
+    diamond_row(rw, d0, d1);
+    const long long g0 = a0 + d0, g1 = a1 + d1;
+    if (g0 < 0 || g0 >= I0 || g1 < 0 || g1 >= I1) continue;
+    const long long h = R - (d0 < 0 ? -d0 : d0) - (d1 < 0 ? -d1 : d1);
+    const long long lo2 = max(a2 - h, 0LL), hi2 = min(a2 + h, I2 - 1);
+    for (long long g2 = lo2 + lane; g2 <= hi2; g2 += 64) f(g0, g1, g2);
+  }
+}
+
 // CG iteration it, part A, for column j = blockIdx.y of a batch: beta from the last residual
 // norms, p_it = r + beta p_{it-1} (computed for the neighbours on the fly, written for this
 // thread's own node), q = (S + eps I) p_it and the partials of p_it . q.  Converged
 // (|r|^2 <= tol2) -> every block of the column returns; block 0 records it.  The launch covers
 // the active cube (np_prev: the grid of the previous B launch, whose partials hold |r_it|^2).
+template <bool OCT>
 __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I0, long long I1,
                                                           long long I2, const int* offs, int m1,
                                                           int srad, const int* slots,
@@ -760,17 +820,14 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   const ActiveCube q = active_cube(w, I1, I2, slots[blockIdx.y], centers[blockIdx.y], it, srad);
   const int m = m1 + 1;
   double acc = 0.0;
-  for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
-       t += (long long)gridDim.x * CG_T) {
-    const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
-                    g2 = q.c2 + t % q.e2;
+  auto node = [&](long long g0, long long g1, long long g2) {
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     const double pi = it == 0 ? cc.r[l] : fma(beta, pold[l], cc.r[l]);
     const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * coef_stride(m);
     double s = c[0] * pi;
     for (int o = 0; o < m1; ++o) {
       const double cv = c[1 + o];
-      if (cv == 0.0) continue;  // outside the grid
+      if (cv == 0.0) continue;  // outside the grid (inner loop: continue is the o-loop's)
       const long long j0 = g0 + offs[3 * o] - q.lo0, j1 = g1 + offs[3 * o + 1] - q.lo1,
                       j2 = g2 + offs[3 * o + 2] - q.lo2;
       if (j0 < 0 || j0 >= w.b0 || j1 < 0 || j1 >= w.b1 || j2 < 0 || j2 >= w.b2) continue;
@@ -781,14 +838,16 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
     pnew[l] = pi;
     cc.q[l] = s;
     acc = fma(pi, s, acc);
-  }
+  };
+  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, node);
   block_partial(acc, cc.part_pq, red);
 }
 
 // CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2
 // (same grid and cube as part A; x = the column slot's box vector).
-__global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I1, long long I2,
-                                                          int srad, const int* slots,
+template <bool OCT>
+__global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I0, long long I1,
+                                                          long long I2, int srad, const int* slots,
                                                           const long long* centers, int it) {
   __shared__ double red[CG_T / 64];
   const CGCol cc = cg_col(w, blockIdx.y);
@@ -800,139 +859,130 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
   double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
   const ActiveCube q = active_cube(w, I1, I2, slot, centers[blockIdx.y], it, srad);
   double acc = 0.0;
-  for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
-       t += (long long)gridDim.x * CG_T) {
-    const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
-                    g2 = q.c2 + t % q.e2;
+  auto node = [&](long long g0, long long g1, long long g2) {
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     x[l] = fma(alpha, p[l], x[l]);
     const double ri = fma(-alpha, cc.q[l], cc.r[l]);
     cc.r[l] = ri;
     acc = fma(ri, ri, acc);
-  }
+  };
+  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, node);
   block_partial(acc, cc.part_rr, red);
 }
 
-// The B best keys (value, then lower index) of `cnt` candidates, one workgroup: B rounds of a
-// block arg-max, each excluding the keys already taken.  key(i) -> (value, index); ties cannot
-// reorder because key_gt is a strict total order on distinct indices.
-template <class KeyFn>
-__device__ int block_topb(int cnt, int B, KeyFn key, double* sv, long long* si, long long* out_idx,
-                          int* out_pos, unsigned char* taken) {
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  for (int i = t; i < cnt; i += SEL_THREADS) taken[i] = 0;
-  __syncthreads();
-  int got = 0;
+// Top-B selection in one workgroup (the refinement batch of a stalled round).  Keys order by
+// value, then LOWER index (key_gt: a strict total order on distinct indices, so every selection
+// below is exact).  A wave extracts the B best of the items its lanes hold by B wave arg-maxes,
+// each removing the winner from its lane; the 16 waves' lists are then merged the same way by
+// wave 0.  (Round 3's version ran B block-wide arg-maxes with two barriers each per level: 750 us
+// for B = 32.)
+template <int P>
+__device__ __forceinline__ void wave_topb(double (&v)[P], long long (&id)[P], int B, double* ov,
+                                          long long* oi) {
+  const int lane = threadIdx.x & 63;
   for (int b = 0; b < B; ++b) {
-    double v = 0.0;
-    long long idx = -1;
-    int pos = -1;
-    for (int i = t; i < cnt; i += SEL_THREADS) {
-      if (taken[i]) continue;
-      double kv;
-      long long ki;
-      key(i, kv, ki);
-      if (key_gt(kv, ki, v, idx)) {
-        v = kv;
-        idx = ki;
-        pos = i;
-      }
-    }
-    // reduce (value, index, position): position rides along with the winning index
+    double bv = 0.0;
+    long long bi = -1;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(v, o, 64);
-      const long long oi = __shfl_xor(idx, o, 64);
-      const int op = __shfl_xor(pos, o, 64);
-      if (key_gt(ov, oi, v, idx)) {
-        v = ov;
-        idx = oi;
-        pos = op;
+    for (int p = 0; p < P; ++p)
+      if (key_gt(v[p], id[p], bv, bi)) {
+        bv = v[p];
+        bi = id[p];
       }
-    }
+    wave_keymax(bv, bi);
     if (lane == 0) {
-      sv[wave] = v;
-      si[wave] = idx;
-      out_pos[CG_B + wave] = pos;
+      ov[b] = bv;
+      oi[b] = bi;
     }
-    __syncthreads();
-    if (t == 0) {
-      double bv = 0.0;
-      long long bi = -1;
-      int bp = -1;
-      for (int k = 0; k < SEL_THREADS / 64; ++k)
-        if (key_gt(sv[k], si[k], bv, bi)) {
-          bv = sv[k];
-          bi = si[k];
-          bp = out_pos[CG_B + k];
-        }
-      out_idx[b] = bi;
-      out_pos[b] = bp;
-      if (bp >= 0) taken[bp] = 1;
-    }
-    __syncthreads();
-    if (out_idx[b] < 0) break;
-    ++got;
+    if (bi < 0) continue;  // fewer than B items: the rest stay -1
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+      if (id[p] == bi) id[p] = -1;
   }
-  __syncthreads();
-  return got;
 }
 
-// The B best cache entries over V \ A: the B best superblocks contain them, the B best blocks of
-// those contain them, so three small top-B passes in one workgroup find them.  out[0] = count,
-// out[1 ..] = the candidates, best first (out[1] is the arg-max).  The whole workgroup calls it.
+// The B best of `count` items (key(i, v, idx), i < count <= P * SEL_THREADS) -> out[0] = how many
+// (<= B), out[1 ..] = their indices, best first.  sv / si: LDS scratch [16 B].  Whole workgroup.
+template <int P, class KeyFn>
+__device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long long* si,
+                               long long* out) {
+  const int t = threadIdx.x, wave = t >> 6;
+  constexpr int NW = SEL_THREADS / 64;
+  double v[P];
+  long long id[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int i = t + p * SEL_THREADS;
+    v[p] = 0.0;
+    id[p] = -1;
+    if (i < count) key(i, v[p], id[p]);
+  }
+  wave_topb<P>(v, id, B, sv + wave * B, si + wave * B);
+  __syncthreads();
+  if (wave == 0) {
+    constexpr int Q = (NW * CG_B + 63) / 64;
+    double v2[Q];
+    long long id2[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = (t & 63) + 64 * q;
+      v2[q] = i < NW * B ? sv[i] : 0.0;
+      id2[q] = i < NW * B ? si[i] : -1;
+    }
+    wave_topb<Q>(v2, id2, B, sv + NW * CG_B, si + NW * CG_B);
+    if ((t & 63) == 0) {
+      int c = 0;
+      for (int b = 0; b < B; ++b) {
+        const long long k = si[NW * CG_B + b];
+        if (k < 0) break;
+        out[1 + c++] = k;
+      }
+      out[0] = c;
+    }
+  }
+  __syncthreads();
+  return (int)out[0];
+}
+
+// The B best cache entries over V \ A: they lie in the B best blocks, which lie in the B best
+// superblocks (a key is its range's maximum).  Keys carry the candidate index, so a selected key
+// names its block (y / EB) and superblock (y / (EB ESB)).  out[0] = count, out[1 ..] = the
+// candidates, best first (out[1] is the arg-max).  The whole workgroup calls it.
 __device__ void block_topb_entries(const double* cache, const unsigned char* sel, long long n,
                                    const ExactWS& w, long long nblk, long long nsb, int B,
                                    long long* out) {
-  __shared__ double sv[SEL_THREADS / 64];
-  __shared__ long long si[SEL_THREADS / 64];
-  __shared__ long long tidx[CG_B];
-  __shared__ int tpos[CG_B + SEL_THREADS / 64];
-  __shared__ long long sbs[CG_B], blks[CG_B];
-  __shared__ unsigned char taken[CG_B * EB > ESB * CG_B ? CG_B * EB : ESB * CG_B];
-  __shared__ int nsbk, nblkk;
-  // superblocks whose key is one of the B best (nsb may exceed the LDS flags: scan by key)
-  if (nsb <= (long long)sizeof(taken)) {
-    const int g = block_topb((int)nsb, B, [&](int i, double& v, long long& k) {
-      v = w.sval[i];
-      k = w.sidx[i];
-    }, sv, si, tidx, tpos, taken);
-    if (threadIdx.x == 0) {
-      nsbk = g;
-      for (int b = 0; b < g; ++b) sbs[b] = tpos[b];
-    }
-  } else if (threadIdx.x == 0) {
-    nsbk = 0;  // (the caller falls back to the arg-max alone)
+  constexpr int NW = SEL_THREADS / 64;
+  __shared__ double sv[NW * CG_B + CG_B];
+  __shared__ long long si[NW * CG_B + CG_B];
+  __shared__ long long sbs[CG_B + 1], blks[CG_B + 1];
+  // superblocks (nsb <= 8 SEL_THREADS: 134 M candidates)
+  auto skey = [&](int i, double& v, long long& k) {
+    v = w.sval[i];
+    k = w.sidx[i];
+  };
+  int ns = 0;
+  if (nsb <= SEL_THREADS) ns = block_topb_keys<1>((int)nsb, B, skey, sv, si, sbs);
+  else if (nsb <= 8 * SEL_THREADS) ns = block_topb_keys<8>((int)nsb, B, skey, sv, si, sbs);
+  if (ns == 0) {  // (no candidate, or too many superblocks: the caller falls back to the arg-max)
+    if (threadIdx.x == 0) out[0] = 0;
+    __syncthreads();
+    return;
   }
-  __syncthreads();
-  const int ns = nsbk;
-  // blocks of those superblocks
-  const int g2 = block_topb(ns * ESB, B, [&](int i, double& v, long long& k) {
-    const long long b = sbs[i / ESB] * ESB + (i % ESB);
+  // blocks of those superblocks (their keys' candidates name them)
+  const int nb = block_topb_keys<2>(ns * ESB, B, [&](int i, double& v, long long& k) {
+    const long long b = (sbs[1 + i / ESB] / (EB * ESB)) * ESB + (i % ESB);
     v = b < nblk ? w.bval[b] : 0.0;
     k = b < nblk ? w.bidx[b] : -1;
-  }, sv, si, tidx, tpos, taken);
-  if (threadIdx.x == 0) {
-    nblkk = g2;
-    for (int b = 0; b < g2; ++b) blks[b] = sbs[tpos[b] / ESB] * ESB + (tpos[b] % ESB);
-  }
-  __syncthreads();
-  const int nbk = nblkk;
+  }, sv, si, blks);
   // entries of those blocks
-  const int g3 = block_topb(nbk * EB, B, [&](int i, double& v, long long& k) {
-    const long long y = blks[i / EB] * EB + (i % EB);
+  block_topb_keys<8>(nb * EB, B, [&](int i, double& v, long long& k) {
+    const long long y = (blks[1 + i / EB] / EB) * EB + (i % EB);
     const bool ok = y < n && !sel[y];
     v = ok ? cache[y] : 0.0;
     k = ok ? y : -1;
-  }, sv, si, tidx, tpos, taken);
-  if (threadIdx.x == 0) {
-    out[0] = g3;
-    for (int b = 0; b < g3; ++b) out[1 + b] = tidx[b];
-  }
-  __syncthreads();
+  }, sv, si, out);
 }
 
-// Device-side rounds, control block reset (the start of a bounded-lazy run).
 __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int nslots) {
   const int t = threadIdx.x;
   if (t < CTL_N) w.ctl[t] = t == CTL_STALL ? -1 : 0;
@@ -947,93 +997,6 @@ __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int n
   }
 }
 
-// One round of the bounded-lazy rounds, decided on the device (vgposp_exact_steps): the arg-max
-// of the cache; if its Q_yy is exact (a refined candidate, its CG column in a slot) it is picked
-// (marked selected, its cache entry 0, its keys refreshed); otherwise the round STALLS: ctl[STALL] = round, and the B best
-// cache entries that have no column yet become the pending refinement batch (rf_cand / rf_slot,
-// ctl[NB]), each given a free slot or the oldest unpinned one — the host loop's rule
-// (sparse_placement.ExactWindowGreedy.run_bounded, round 3).  Every later kernel of the rounds
-// sees the stall (picks[round] stays -1, ctl[STALL] >= 0) and does nothing, until the host has
-// run the refinement (exact_refine_end_kernel clears the stall) and re-issues the rounds from
-// the stalled one.  One workgroup.
-__global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(double* cache, unsigned char* sel,
-                                                                 long long n, ExactWS w,
-                                                                 long long nblk, long long nsb,
-                                                                 int nslots, int round, int B,
-                                                                 long long* picks,
-                                                                 double* pick_delta) {
-  __shared__ int s_slot;
-  __shared__ long long top[CG_B + 1];
-  if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
-  const long long a = block_argmax(w, nsb);
-  if (threadIdx.x == 0) s_slot = -1;
-  __syncthreads();
-  if (a >= 0)
-    for (int i = threadIdx.x; i < nslots; i += SEL_THREADS)
-      if (w.rl_cand[i] == a) s_slot = i;
-  __syncthreads();
-  const int slot = s_slot;
-  if (a < 0 || slot >= 0) {  // pick (no candidate left: picks[round] = -1, nothing changes)
-    if (threadIdx.x == 0) {
-      picks[round] = a;
-      if (pick_delta) pick_delta[round] = a >= 0 ? cache[a] : 0.0;
-      if (a >= 0) {
-        w.slot_of_round[round] = slot;
-        w.rl_pin[slot] = 1;
-        w.ctl[CTL_UNPICKED] -= 1;
-        sel[a] = 1;
-        cache[a] = 0.0;
-      }
-    }
-    __syncthreads();
-    if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
-    return;
-  }
-  // stall: the B best entries without a column become the refinement batch
-  block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
-  if (threadIdx.x == 0) {
-    long long todo[CG_B];
-    int nt = 0;
-    for (int b = 0; b < (int)top[0]; ++b) {
-      const long long y = top[1 + b];
-      bool has = false;
-      for (int i = 0; i < nslots; ++i) has = has || w.rl_cand[i] == y;
-      if (!has) todo[nt++] = y;
-    }
-    if (nt == 0) todo[nt++] = a;
-    int nb = 0;
-    for (int j = 0; j < nt; ++j) {
-      int slot_j = -1;
-      for (int i = 0; i < nslots && slot_j < 0; ++i)
-        if (w.rl_cand[i] < 0) slot_j = i;  // a free slot (lowest first)
-      if (slot_j < 0) {  // recycle the oldest refined candidate not picked and not in the batch
-        int best_age = 0x7fffffff;
-        for (int i = 0; i < nslots; ++i) {
-          if (w.rl_pin[i]) continue;
-          bool in_batch = false;
-          for (int q = 0; q < nt; ++q) in_batch = in_batch || todo[q] == w.rl_cand[i];
-          if (!in_batch && w.rl_age[i] < best_age) {
-            best_age = w.rl_age[i];
-            slot_j = i;
-          }
-        }
-        if (slot_j < 0) break;
-        w.ctl[CTL_UNPICKED] -= 1;  // its candidate loses its column (it is bounded again)
-      }
-      w.rl_cand[slot_j] = todo[j];
-      w.rl_age[slot_j] = w.ctl[CTL_AGE]++;
-      w.rf_cand[nb] = todo[j];
-      w.rf_slot[nb] = slot_j;
-      ++nb;
-    }
-    for (int j = nb; j < CG_B; ++j) {
-      w.rf_cand[j] = -1;
-      w.rf_slot[j] = -1;
-    }
-    w.ctl[CTL_NB] = nb;
-    w.ctl[CTL_STALL] = round;
-  }
-}
 
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
 
@@ -1116,38 +1079,41 @@ __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRow
 
 // Bounded-lazy path, after the CG columns of the batch (cands[j] in slots[j], j < nb): each Q_cc
 // is now known; the candidate's cache entry becomes the reference's value (scored with the A of
-// its last re-score) and its keys are refreshed.  One wave, the batch in order (two candidates may
-// share a key block).
+// its last re-score) and its keys are refreshed.  One workgroup: the candidates are re-scored one
+// wave each, then the block keys of their blocks (two candidates may share one: both waves write
+// the same key from the same cache) and after a barrier the superblock keys.
 template <int KIND>
-__global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* qdiag,
-                                                              double* cache, unsigned char* sel,
-                                                              ExactWS w, long long nblk, int nb,
-                                                              const int* slots,
-                                                              const long long* cands,
-                                                              const long long* picks,
-                                                              int resume) {
-  int done = 0;
-  for (int j = 0; j < nb; ++j) {
+__global__ __launch_bounds__(SEL_THREADS) void exact_refine_end_kernel(EArgs a, double* qdiag,
+                                                                       double* cache,
+                                                                       unsigned char* sel,
+                                                                       ExactWS w, long long nblk,
+                                                                       int nb, const int* slots,
+                                                                       const long long* cands,
+                                                                       const long long* picks,
+                                                                       int resume) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int NWAVE = SEL_THREADS / 64;
+  for (int j = wave; j < nb; j += NWAVE) {
     const long long c = cands[j];
     if (c < 0) continue;
-    ++done;
     const double qcc = qslot_at(w, slots[j], c, a.I1, a.I2);
     const double d = wave_rescore<KIND>(a, w, global_rows(w, a.kmax), picks, (int)w.lastA[c], c,
                                         qcc, true);
-    if (threadIdx.x == 0) {
+    if (lane == 0) {
       qdiag[c] = qcc;
       w.qexact[c] = 1;
       cache[c] = d;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    wave_refresh_keys(cache, sel, w, a.n, nblk, c);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  __syncthreads();
+  for (int j = wave; j < nb; j += NWAVE)
+    if (cands[j] >= 0) wave_block_key(cache, sel, a.n, cands[j] / EB, w.bval, w.bidx);
+  __syncthreads();
+  for (int j = wave; j < nb; j += NWAVE)
+    if (cands[j] >= 0) wave_super_key(w.bval, w.bidx, nblk, cands[j] / EB / ESB, w.sval, w.sidx);
   if (resume && threadIdx.x == 0) {  // device-side rounds: the stalled round may go on
+    int done = 0;
+    for (int j = 0; j < nb; ++j) done += cands[j] >= 0;
     w.ctl[CTL_UNPICKED] += done;
     w.ctl[CTL_REFINED] += done;
     w.ctl[CTL_EVENTS] += 1;
@@ -1160,16 +1126,18 @@ __global__ __launch_bounds__(64) void exact_refine_end_kernel(EArgs a, double* q
 // at once, then one forward substitution with lane s holding z_s).
 constexpr int ROWS_LDS = 8192;  // doubles: packed rows of both factors up to |A| = 63
 
+// Row `round` of both factors, the whole workgroup (>= 128 threads) calling: waves 0 and 1 compute
+// (LQ / LS), every thread stages the earlier rows.
 template <int KIND>
-__global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int round,
-                                                         const long long* picks) {
-  __shared__ double sm[ROWS_LDS];
+__device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
+                                  const long long* picks, double* sm) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int km = a.kmax;
   const long long at = picks[round];
   if (at < 0) return;
   const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, km, round, sm)
                                                         : global_rows(w, km);
+  if (wave > 1) return;
   const double* Lm = wave == 0 ? L.lq : L.ls;
   auto val = [&](int r) {
     if (wave == 0) return qcol_at(w, round, picks[r], a.I1, a.I2);
@@ -1197,6 +1165,13 @@ __global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int
   // diagonal: sqrt(v_round - |z|^2), v_round held by lane round % 64
   const double vr = __shfl(round < 64 ? v0 : v1, round & 63, 64);
   if (lane == 0) Lw[round] = sqrt(vr - nz);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int round,
+                                                         const long long* picks) {
+  __shared__ double sm[ROWS_LDS];
+  block_factor_rows<KIND>(a, w, round, picks, sm);
 }
 
 struct Window {
@@ -1246,7 +1221,27 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
 }
 
 // Part 3: refresh the block keys of the window rows (each (j0, j1) row is one contiguous i2 run),
-// then their superblock keys.  One workgroup.
+// then their superblock keys.  The whole workgroup calls it (at >= 0: the window's centre).
+__device__ void block_window_keys(const EArgs& a, const double* cache, const unsigned char* sel,
+                                  const ExactWS& w, long long nblk, long long at) {
+  const Window v = window_of(a, at);
+  const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
+  const long long nrow = v.w0 * v.w1;
+  for (long long rr = wave; rr < nrow; rr += nwave) {
+    const long long y0 = ((v.lo0 + rr / v.w1) * a.I1 + v.lo1 + rr % v.w1) * a.I2 + v.lo2;
+    const long long y1 = y0 + v.w2 - 1;
+    for (long long b = y0 / EB; b <= y1 / EB; ++b) wave_block_key(cache, sel, a.n, b, w.bval, w.bidx);
+  }
+  __syncthreads();
+  for (long long rr = wave; rr < nrow; rr += nwave) {
+    const long long y0 = ((v.lo0 + rr / v.w1) * a.I1 + v.lo1 + rr % v.w1) * a.I2 + v.lo2;
+    const long long y1 = y0 + v.w2 - 1;
+    for (long long sb = y0 / EB / ESB; sb <= y1 / EB / ESB; ++sb)
+      wave_super_key(w.bval, w.bidx, nblk, sb, w.sval, w.sidx);
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(SEL_THREADS) void exact_window_keys_kernel(EArgs a, const double* cache,
                                                                         const unsigned char* sel,
                                                                         ExactWS w, long long nblk,
@@ -1268,6 +1263,103 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_window_keys_kernel(EArgs a,
     const long long y1 = y0 + v.w2 - 1;
     for (long long sb = y0 / EB / ESB; sb <= y1 / EB / ESB; ++sb)
       wave_super_key(w.bval, w.bidx, nblk, sb, w.sval, w.sidx);
+  }
+}
+
+// One round of the bounded-lazy rounds, decided on the device (vgposp_exact_steps).  First the
+// keys of the previous round's window (its re-scored cache entries), then the arg-max of the
+// cache; if its Q_yy is exact (a refined candidate, its CG column in a slot) it is picked (marked
+// selected, its cache entry 0, its keys refreshed) and, with `rows`, the pick's rows of
+// chol(Q_AA) and chol(S_AA + eps I) are appended; otherwise the round STALLS: ctl[STALL] = round,
+// and the B best cache entries that have no column yet become the pending refinement batch
+// (rf_cand / rf_slot, ctl[NB]), each given a free slot or the oldest unpinned one — the host
+// loop's rule (sparse_placement.ExactWindowGreedy.run_bounded, round 3).  Every later kernel of
+// the issued rounds sees the stall (picks[round] stays -1, ctl[STALL] >= 0) and does nothing,
+// until the host has run the refinement (exact_refine_end_kernel clears the stall) and re-issues
+// the rounds from the stalled one.  One workgroup; a round is this kernel plus the window
+// re-score (exact_window_kernel).
+template <int KIND>
+__global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, double* cache,
+                                                                 unsigned char* sel, ExactWS w,
+                                                                 long long nblk, long long nsb,
+                                                                 int nslots, int round, int B,
+                                                                 int rows, long long* picks,
+                                                                 double* pick_delta) {
+  __shared__ int s_slot;
+  __shared__ long long top[CG_B + 1];
+  __shared__ double sm[ROWS_LDS];
+  if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
+  const long long n = ea.n;
+  if (round > 0 && picks[round - 1] >= 0)
+    block_window_keys(ea, cache, sel, w, nblk, picks[round - 1]);
+  const long long a = block_argmax(w, nsb);
+  if (threadIdx.x == 0) s_slot = -1;
+  __syncthreads();
+  if (a >= 0)
+    for (int i = threadIdx.x; i < nslots; i += SEL_THREADS)
+      if (w.rl_cand[i] == a) s_slot = i;
+  __syncthreads();
+  const int slot = s_slot;
+  if (a < 0 || slot >= 0) {  // pick (no candidate left: picks[round] = -1, nothing changes)
+    if (threadIdx.x == 0) {
+      picks[round] = a;
+      if (pick_delta) pick_delta[round] = a >= 0 ? cache[a] : 0.0;
+      if (a >= 0) {
+        w.slot_of_round[round] = slot;
+        w.rl_pin[slot] = 1;
+        w.ctl[CTL_UNPICKED] -= 1;
+        sel[a] = 1;
+        cache[a] = 0.0;
+      }
+    }
+    __syncthreads();
+    if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
+    if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm);
+    return;
+  }
+  // stall: the B best entries without a column become the refinement batch
+  block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
+  if (threadIdx.x == 0) {
+    long long todo[CG_B];
+    int nt = 0;
+    for (int b = 0; b < (int)top[0]; ++b) {
+      const long long y = top[1 + b];
+      bool has = false;
+      for (int i = 0; i < nslots; ++i) has = has || w.rl_cand[i] == y;
+      if (!has) todo[nt++] = y;
+    }
+    if (nt == 0) todo[nt++] = a;
+    int nb = 0;
+    for (int j = 0; j < nt; ++j) {
+      int slot_j = -1;
+      for (int i = 0; i < nslots && slot_j < 0; ++i)
+        if (w.rl_cand[i] < 0) slot_j = i;  // a free slot (lowest first)
+      if (slot_j < 0) {  // recycle the oldest refined candidate not picked and not in the batch
+        int best_age = 0x7fffffff;
+        for (int i = 0; i < nslots; ++i) {
+          if (w.rl_pin[i]) continue;
+          bool in_batch = false;
+          for (int q = 0; q < nt; ++q) in_batch = in_batch || todo[q] == w.rl_cand[i];
+          if (!in_batch && w.rl_age[i] < best_age) {
+            best_age = w.rl_age[i];
+            slot_j = i;
+          }
+        }
+        if (slot_j < 0) break;
+        w.ctl[CTL_UNPICKED] -= 1;  // its candidate loses its column (it is bounded again)
+      }
+      w.rl_cand[slot_j] = todo[j];
+      w.rl_age[slot_j] = w.ctl[CTL_AGE]++;
+      w.rf_cand[nb] = todo[j];
+      w.rf_slot[nb] = slot_j;
+      ++nb;
+    }
+    for (int j = nb; j < CG_B; ++j) {
+      w.rf_cand[j] = -1;
+      w.rf_slot[j] = -1;
+    }
+    w.ctl[CTL_NB] = nb;
+    w.ctl[CTL_STALL] = round;
   }
 }
 
@@ -1370,17 +1462,31 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int nb, const int* slots,
                      dim3(256), 0, s, w, a.I0, a.I1, a.I2, slots, centers);
   VG_LAUNCH_CHECK();
   const double tol2 = cg_tol * cg_tol;
+  // the 7-point stencil (face neighbours only): walk the Manhattan ball, not its bounding cube
+  const bool oct = a.m1 == 6 && radius == 1;  // (the 6 offsets of squared distance 1)
   unsigned prev = 1;
   for (int it = 0; it < cg_iters; ++it) {
-    // the unclipped active cube bounds the launch: a grid that grows with the iterate's support
+    // the unclipped active region bounds the launch: a grid that grows with the iterate's support
     const long long side = std::min<long long>(2LL * (it + 1) * radius + 1, 2 * w.H + 1);
-    const unsigned blocks =
-        (unsigned)std::min<long long>(CG_BLOCKS, ceil_div(side * side * side, (long long)CG_T));
-    hipLaunchKernelGGL(exact_cg_a_kernel, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w, a.I0,
-                       a.I1, a.I2, a.offs, a.m1, radius, slots, centers, it, (int)prev, tol2);
-    VG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(exact_cg_b_kernel, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w, a.I1,
-                       a.I2, radius, slots, centers, it);
+    const long long R = std::min<long long>(it + 1, w.H);
+    const unsigned blocks = (unsigned)std::min<long long>(
+        CG_BLOCKS, oct ? ceil_div(2 * R * R + 2 * R + 1, (long long)(CG_T / 64))
+                       : ceil_div(side * side * side, (long long)CG_T));
+    if (oct) {
+      hipLaunchKernelGGL(exact_cg_a_kernel<true>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
+                         a.I0, a.I1, a.I2, a.offs, a.m1, radius, slots, centers, it, (int)prev,
+                         tol2);
+      VG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(exact_cg_b_kernel<true>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
+                         a.I0, a.I1, a.I2, radius, slots, centers, it);
+    } else {
+      hipLaunchKernelGGL(exact_cg_a_kernel<false>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
+                         a.I0, a.I1, a.I2, a.offs, a.m1, radius, slots, centers, it, (int)prev,
+                         tol2);
+      VG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(exact_cg_b_kernel<false>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
+                         a.I0, a.I1, a.I2, radius, slots, centers, it);
+    }
     VG_LAUNCH_CHECK();
     prev = blocks;
   }
@@ -1434,7 +1540,7 @@ int exact_refine_t(const EArgs& a, double* qdiag, double* cache, unsigned char* 
                    int resume = 0) {
   const long long nblk = ceil_div(a.n, EB);
   if (int rc = exact_cg_run(a, w, nb, slots, cands, radius, cg_iters, cg_tol, s)) return rc;
-  hipLaunchKernelGGL(exact_refine_end_kernel<KIND>, dim3(1), dim3(64), 0, s, a, qdiag, cache, sel, w,
+  hipLaunchKernelGGL(exact_refine_end_kernel<KIND>, dim3(1), dim3(SEL_THREADS), 0, s, a, qdiag, cache, sel, w,
                      nblk, nb, slots, cands, picks, resume);
   VG_LAUNCH_CHECK();
   return 0;
@@ -1553,29 +1659,37 @@ extern "C" int vgposp_exact_steps_reset(VGPOSP_EXACT_PARAMS, void* stream) {
   return 0;
 }
 
-extern "C" int vgposp_exact_steps(VGPOSP_EXACT_PARAMS, int round0, int round1, int batch,
+extern "C" int vgposp_exact_steps(VGPOSP_EXACT_PARAMS, int round0, int round1, int k, int batch,
                                   int64_t* picks, double* pick_delta, void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_steps");
-  VG_CHECK_ARG(round0 >= 0 && round0 <= round1 && round1 <= kmax, 24);
-  VG_CHECK_ARG(batch >= 1 && batch <= CG_B, 26);
-  VG_CHECK_ARG(picks != nullptr, 27);
+  VG_CHECK_ARG(k >= 1 && k <= kmax, 26);
+  VG_CHECK_ARG(round0 >= 0 && round0 <= round1 && round1 <= k, 24);
+  VG_CHECK_ARG(batch >= 1 && batch <= CG_B, 27);
+  VG_CHECK_ARG(picks != nullptr, 28);
   const long long nblk = ceil_div(a.n, EB), nsb = ceil_div(nblk, ESB);
   long long* pk = reinterpret_cast<long long*>(picks);
-  for (int r = round0; r < round1; ++r) {
-    {
-      ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
-      hipLaunchKernelGGL(exact_step_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
-                         nblk, nsb, exact_slots(kmax), r, batch, pk, pick_delta);
-      VG_LAUNCH_CHECK();
+  const long long side = 2LL * a.cutoff;
+  const long long nw = side * side * side;
+  return dispatch_kind(kind, [&](auto K) {
+    constexpr int KD = decltype(K)::value;
+    for (int r = round0; r < round1; ++r) {
+      const bool more = r + 1 < k;  // the last pick needs neither factor rows nor a window
+      {
+        ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
+        hipLaunchKernelGGL(exact_step_kernel<KD>, dim3(1), dim3(SEL_THREADS), 0, s, a, cache,
+                           selected, w, nblk, nsb, exact_slots(kmax), r, batch, (int)more, pk,
+                           pick_delta);
+        VG_LAUNCH_CHECK();
+      }
+      if (more && nw > 0) {  // the window of pick r (no-op when the round stalled: picks[r] = -1)
+        ProfScope ps("exact_update", s, 0.0, 0.0);
+        hipLaunchKernelGGL(exact_window_kernel<KD>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, s,
+                           a, qdiag, cache, selected, w, r, pk);
+        VG_LAUNCH_CHECK();
+      }
     }
-    if (r + 1 < kmax) {  // the window of pick r (no-op when the round stalled: picks[r] = -1)
-      const int rc = dispatch_kind(kind, [&](auto K) {
-        return exact_update_t<decltype(K)::value>(a, qdiag, cache, selected, w, r, pk, s);
-      });
-      if (rc) return rc;
-    }
-  }
-  return 0;
+    return 0;
+  });
 }
 
 extern "C" int vgposp_exact_refine_pending(VGPOSP_EXACT_PARAMS, int batch, const int64_t* picks,

@@ -407,7 +407,9 @@ def cg_iterations_for(lam_min, lam_max, tol=1e-16):
 
 
 BOUND_TMAX, BOUND_NBMAX = 14 * 64, 8192
-REFINE_BATCH = 8        # candidates refined together by one batched CG (vgposp_exact_refine)     # exact_bounds_kernel's register / LDS tables
+REFINE_BATCH = 32       # candidates refined together by one batched CG (vgposp_exact_refine_pending);
+#                         measured at 128^3: batch 8 14.3 ms, 16 13.4, 32 12.4 (profiles/r4_c4_batch_*)
+REFINE_BATCH_MAX = 32   # the library's CG_B
 BOUND_MARGIN = 1e-12                       # relative rounding margin on the upper bounds
 
 
@@ -541,8 +543,8 @@ class ExactWindowGreedy:
         if k > self.kmax:
             raise ValueError(f"k = {k} > kmax = {self.kmax}")
         B = REFINE_BATCH if batch is None else int(batch)
-        if not 1 <= B <= 8:
-            raise ValueError(f"batch must be in [1, 8], got {B}")
+        if not 1 <= B <= REFINE_BATCH_MAX:
+            raise ValueError(f"batch must be in [1, {REFINE_BATCH_MAX}], got {B}")
         self.picks.fill_(-1)
         args = self._args(qdiag)
         st = _stream()
@@ -550,7 +552,7 @@ class ExactWindowGreedy:
         call("vgposp_exact_steps_reset", *args, st)
         ctl = self._ctl()
         pk, pd = _p(self.picks), _p(self.pick_delta)
-        call("vgposp_exact_steps", *args, 0, 1, B, pk, pd, st)  # round 0 stalls: nothing refined
+        call("vgposp_exact_steps", *args, 0, 1, k, B, pk, pd, st)  # round 0 stalls: nothing refined
         issued, reads = 1, 0
         while True:
             c = ctl.cpu().tolist()  # stall round, batch size, refined-unpicked, events, refined
@@ -563,7 +565,7 @@ class ExactWindowGreedy:
                 r0, r1 = issued, min(k, issued + max(c[2], 0) + 1)
             else:
                 break
-            call("vgposp_exact_steps", *args, r0, r1, B, pk, pd, st)
+            call("vgposp_exact_steps", *args, r0, r1, k, B, pk, pd, st)
             issued = r1
         self.refinements, self.refine_batches, self.host_reads = c[4], c[3], reads
         return self.picks[:k]
