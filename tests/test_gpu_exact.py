@@ -107,7 +107,8 @@ def test_bounded_alg3_matches_oracle(shape, k, cutoff, beta, kind):
     np.testing.assert_allclose(run.greedy.pick_delta[:k].cpu().numpy(),
                                [rdci[a, i] for i, a in enumerate(rA)], rtol=1e-10)
     g = run.greedy
-    assert g.refine_batches <= 2 * k and k <= g.refinements <= 8 * g.refine_batches
+    from vgposp_amd.sparse_placement import REFINE_BATCH
+    assert g.refine_batches <= 2 * k and k <= g.refinements <= REFINE_BATCH * g.refine_batches
 
 
 @pytest.mark.parametrize("shape,k,cutoff", [
