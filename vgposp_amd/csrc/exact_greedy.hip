@@ -999,6 +999,7 @@ __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int n
 
 
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
+constexpr int EX_SLOTS_MAX = 2 * EX_KMAX;  // column slots (exact_slots(kmax) <= this)
 
 // Rows of chol(Q_AA) / chol(S_AA + eps I): in the workspace (row stride kmax) or packed lower
 // triangles staged in LDS (row r at r (r + 1) / 2).
@@ -1317,39 +1318,66 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
     if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm);
     return;
   }
-  // stall: the B best entries without a column become the refinement batch
+  // stall: the B best entries without a column become the refinement batch.  The slot table is
+  // staged in LDS and ranked in parallel (a first version walked it with thread 0's dependent
+  // global loads: 750 us per stall at B = 32): free slots are taken first, lowest index first,
+  // then the unpinned ones, oldest refinement first — the candidates in the batch have no column,
+  // so no slot of theirs can be recycled.
   block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
-  if (threadIdx.x == 0) {
+  __shared__ long long s_cand[EX_SLOTS_MAX];
+  __shared__ int s_age[EX_SLOTS_MAX], s_inv_free[EX_SLOTS_MAX], s_inv_old[EX_SLOTS_MAX];
+  __shared__ unsigned char s_pin[EX_SLOTS_MAX];
+  __shared__ int s_has[CG_B], s_nfree, s_nold;
+  const int t = threadIdx.x;
+  if (t < nslots) {
+    s_cand[t] = w.rl_cand[t];
+    s_age[t] = w.rl_age[t];
+    s_pin[t] = w.rl_pin[t];
+  }
+  if (t < CG_B) s_has[t] = 0;
+  if (t == 0) s_nfree = s_nold = 0;
+  __syncthreads();
+  const int ntop = (int)top[0];
+  for (int e = t; e < nslots * ntop; e += SEL_THREADS) {
+    const int i = e / ntop, b = e % ntop;
+    if (s_cand[i] >= 0 && s_cand[i] == top[1 + b]) s_has[b] = 1;
+  }
+  if (t < nslots) {
+    const bool fr = s_cand[t] < 0, old = !fr && !s_pin[t];
+    int rank = 0;
+    for (int i = 0; i < nslots; ++i) {
+      if (fr) rank += s_cand[i] < 0 && i < t;
+      else if (old) rank += s_cand[i] >= 0 && !s_pin[i] && (s_age[i] < s_age[t] || (s_age[i] == s_age[t] && i < t));
+    }
+    if (fr) {
+      s_inv_free[rank] = t;
+      atomicAdd(&s_nfree, 1);
+    } else if (old) {
+      s_inv_old[rank] = t;
+      atomicAdd(&s_nold, 1);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
     long long todo[CG_B];
     int nt = 0;
-    for (int b = 0; b < (int)top[0]; ++b) {
-      const long long y = top[1 + b];
-      bool has = false;
-      for (int i = 0; i < nslots; ++i) has = has || w.rl_cand[i] == y;
-      if (!has) todo[nt++] = y;
-    }
+    for (int b = 0; b < ntop; ++b)
+      if (!s_has[b]) todo[nt++] = top[1 + b];
     if (nt == 0) todo[nt++] = a;
-    int nb = 0;
+    const int nfree = s_nfree, nold = s_nold;
+    int nb = 0, age = w.ctl[CTL_AGE], recycled = 0;
     for (int j = 0; j < nt; ++j) {
-      int slot_j = -1;
-      for (int i = 0; i < nslots && slot_j < 0; ++i)
-        if (w.rl_cand[i] < 0) slot_j = i;  // a free slot (lowest first)
-      if (slot_j < 0) {  // recycle the oldest refined candidate not picked and not in the batch
-        int best_age = 0x7fffffff;
-        for (int i = 0; i < nslots; ++i) {
-          if (w.rl_pin[i]) continue;
-          bool in_batch = false;
-          for (int q = 0; q < nt; ++q) in_batch = in_batch || todo[q] == w.rl_cand[i];
-          if (!in_batch && w.rl_age[i] < best_age) {
-            best_age = w.rl_age[i];
-            slot_j = i;
-          }
-        }
-        if (slot_j < 0) break;
-        w.ctl[CTL_UNPICKED] -= 1;  // its candidate loses its column (it is bounded again)
+      int slot_j;
+      if (j < nfree) {
+        slot_j = s_inv_free[j];
+      } else if (j - nfree < nold) {
+        slot_j = s_inv_old[j - nfree];
+        ++recycled;  // its candidate loses its column (it is bounded again)
+      } else {
+        break;
       }
       w.rl_cand[slot_j] = todo[j];
-      w.rl_age[slot_j] = w.ctl[CTL_AGE]++;
+      w.rl_age[slot_j] = age++;
       w.rf_cand[nb] = todo[j];
       w.rf_slot[nb] = slot_j;
       ++nb;
@@ -1358,6 +1386,8 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
       w.rf_cand[j] = -1;
       w.rf_slot[j] = -1;
     }
+    w.ctl[CTL_AGE] = age;
+    w.ctl[CTL_UNPICKED] -= recycled;
     w.ctl[CTL_NB] = nb;
     w.ctl[CTL_STALL] = round;
   }

@@ -126,7 +126,7 @@ class DistCholesky:
     def _splits(self, nsub):
         return self.world > 1 and nsub >= self.dist_min and nsub > BLOCK_INV
 
-    def _rec(self, col0, nsub):
+    def _rec(self, col0, nsub, depth=0):
         ops = self.ops
         if not self._splits(nsub):
             self._flush(col0, col0 + nsub)
@@ -135,7 +135,7 @@ class DistCholesky:
         n1 = ops.split(nsub)
         n2 = nsub - n1
         base = col0 + n1
-        self._rec(col0, n1)
+        self._rec(col0, n1, depth + 1)
         self._flush(col0, col0 + nsub)     # the panel reads rows [col0, col0 + nsub)
         shares = even_rows(n2, self.world)
         ops.panel(col0, nsub, *shares[self.rank])
@@ -150,8 +150,8 @@ class DistCholesky:
             bands = lower_bands(n2, self.world, start=h)
             ops.trailing(col0, nsub, *bands[self.rank])
             self._exchange([(base + a, base + b, base, base + b, 1) for a, b in bands],
-                           defer=(base + h, base + n2))
-        self._rec(base, n2)
+                           defer=(base + h, base + n2), depth=depth)
+        self._rec(base, n2, depth + 1)
 
     def _buf(self, key, numel, device):
         b = self._bufs.get(key)
@@ -160,10 +160,17 @@ class DistCholesky:
             self._bufs[key] = b
         return b[:numel]
 
-    def _exchange(self, pieces, defer=None):
+    def _exchange(self, pieces, defer=None, depth=0):
         """All-gather every rank's piece (r0, r1, c0, c1, lower) of the matrix.  ``defer`` = the
         row range the pieces cover: the all-gather is issued asynchronously and the received
-        pieces are unpacked by the first _flush that touches those rows."""
+        pieces are unpacked by the first _flush that touches those rows.
+
+        A deferred exchange keeps its buffers until that unpack, i.e. through the whole top-left
+        recursion of the node's bottom-right child (that is the overlap); at most one is pending
+        per recursion depth (a node's is unpacked by its bottom-right child's first flush, before
+        the child issues its own), so each depth reuses one buffer pair.  Peak device memory per
+        rank: the synchronous pair plus one deferred pair per depth, about 2 (1 + 1/R) x the
+        top node's deferred rows (at the 65k top node, rows [h, n2) of A22: ~3 GB per buffer)."""
         ops = self.ops
         sizes = [ops.pack_elems(*p) for p in pieces]
         S = max(sizes)
@@ -172,9 +179,9 @@ class DistCholesky:
         if defer is None:
             send = self._buf("send", S, ops.device)
             recv = self._buf("recv", self.world * S, ops.device)
-        else:  # private buffers: they live until the unpack
-            send = torch.empty(S, dtype=torch.float64, device=ops.device)
-            recv = torch.empty(self.world * S, dtype=torch.float64, device=ops.device)
+        else:  # this depth's pair: it lives until the unpack
+            send = self._buf(("dsend", depth), S, ops.device)
+            recv = self._buf(("drecv", depth), self.world * S, ops.device)
         if sizes[self.rank]:
             ops.pack(*pieces[self.rank], send, False)
         host = None
