@@ -14,3 +14,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o c4 --
 python3 $R/tools/timeline.py $O/tr/c4_kernel_trace.csv --marker exact_gersh_final --step -1 > $O/c4_timeline.txt
 rm -rf $O/tr
 echo ok trace
+cd $R
+VGPOSP_LIB=$R/tools/variants/lib_rr.so timeout -k 10 300 python -u tools/c4_time.py 32 > $O/c4_time_rr.jsonl 2> $O/c4_time_rr.err
+echo ok rr

@@ -289,6 +289,9 @@ __global__ __launch_bounds__(64) void exact_gersh_final_kernel(double* part, int
 // node + off_o or -1); lane l holds nodes l, l + 64, ... in registers, p is exchanged through a
 // wave-private LDS vector.  Step it touches only the tab_cnt[it + 1] nodes A p_it can reach.
 // qhi[y] = hi_scale * sum_i alpha_i |r_i|^2, hi_scale = (1 + margin) / (1 - 4 rho^(2K)).
+#ifndef VGPOSP_BND_RR
+#define VGPOSP_BND_RR 0
+#endif
 constexpr int BND_T = 256;
 constexpr int BND_WAVES = BND_T / 64;
 constexpr int BND_SMAX = 14;
@@ -311,8 +314,18 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double* pl = plds[wave];
   const int m = m1 + 1;
+  // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so XCD x (= blockIdx.x
+  // mod 8) walks its own contiguous eighth of the candidates and neighbouring candidates, whose
+  // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
+#if VGPOSP_BND_RR  // (A/B: the plain round-robin order)
   for (long long y = c0 + (long long)blockIdx.x * BND_WAVES + wave; y < c1;
        y += (long long)gridDim.x * BND_WAVES) {
+#else
+  const long long per_xcd = (c1 - c0 + 7) / 8, xlo = c0 + (blockIdx.x & 7) * per_xcd;
+  const long long xhi = min(c1, xlo + per_xcd);
+  for (long long y = xlo + (long long)(blockIdx.x >> 3) * BND_WAVES + wave; y < xhi;
+       y += (long long)(gridDim.x >> 3) * BND_WAVES) {
+#endif
     const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
     int gi[BND_SMAX];  // grid index (n < 2^31, checked by the caller) or -1
     double r[BND_SMAX], p[BND_SMAX], q[BND_SMAX];
@@ -408,8 +421,18 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
   if (lane == 0) pl[TP] = 0.0;
   __syncthreads();
   constexpr int M = M1 + 1;
+  // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so XCD x (= blockIdx.x
+  // mod 8) walks its own contiguous eighth of the candidates and neighbouring candidates, whose
+  // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
+#if VGPOSP_BND_RR  // (A/B: the plain round-robin order)
   for (long long y = c0 + (long long)blockIdx.x * BND_WAVES + wave; y < c1;
        y += (long long)gridDim.x * BND_WAVES) {
+#else
+  const long long per_xcd = (c1 - c0 + 7) / 8, xlo = c0 + (blockIdx.x & 7) * per_xcd;
+  const long long xhi = min(c1, xlo + per_xcd);
+  for (long long y = xlo + (long long)(blockIdx.x >> 3) * BND_WAVES + wave; y < xhi;
+       y += (long long)(gridDim.x >> 3) * BND_WAVES) {
+#endif
     const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
     double c[SM][M];
     double r[SM], p[SM], q[SM];
@@ -1656,7 +1679,8 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   if (c1 == c0) return 0;
   ProfScope ps("exact_bounds", s, 0.0, 0.0);
   const long long waves = c1 - c0;
-  const unsigned blocks = (unsigned)std::min<long long>(ceil_div(waves, BND_WAVES), 65536);
+  const unsigned blocks =
+      (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES), 8LL), 8192));
   double* out = const_cast<double*>(qdiag);
   const long long lc0 = c0, lc1 = c1;
 #define VG_BOUNDS_REG(SMV)                                                                       \
