@@ -1310,7 +1310,6 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
                                                                  int rows, long long* picks,
                                                                  double* pick_delta) {
   __shared__ int s_slot;
-  __shared__ long long top[CG_B + 1];
   __shared__ double sm[ROWS_LDS];
   if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
   const long long n = ea.n;
@@ -1341,6 +1340,22 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
     if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm);
     return;
   }
+  // stall: the batch is chosen by exact_stall_kernel, which the host launches first thing in
+  // the refinement (vgposp_exact_refine_pending)
+  if (threadIdx.x == 0) w.ctl[CTL_STALL] = round;
+}
+
+// The refinement batch of a stalled round: the B best entries without a column, each given a
+// free slot or the oldest unpinned one (the host loop's rule, ExactWindowGreedy.run_bounded of
+// round 3).  One workgroup.
+__global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache, unsigned char* sel,
+                                                                  long long n, ExactWS w,
+                                                                  long long nblk, long long nsb,
+                                                                  int nslots, int B) {
+  __shared__ long long top[CG_B + 1];
+  __shared__ long long s_todo[CG_B];
+  if (w.ctl[CTL_STALL] < 0) return;
+  const long long a = block_argmax(w, nsb);
   // stall: the B best entries without a column become the refinement batch.  The slot table is
   // staged in LDS and ranked in parallel (a first version walked it with thread 0's dependent
   // global loads: 750 us per stall at B = 32): free slots are taken first, lowest index first,
@@ -1382,7 +1397,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
   }
   __syncthreads();
   if (t == 0) {
-    long long todo[CG_B];
+    long long* todo = s_todo;
     int nt = 0;
     for (int b = 0; b < ntop; ++b)
       if (!s_has[b]) todo[nt++] = top[1 + b];
@@ -1412,7 +1427,6 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
     w.ctl[CTL_AGE] = age;
     w.ctl[CTL_UNPICKED] -= recycled;
     w.ctl[CTL_NB] = nb;
-    w.ctl[CTL_STALL] = round;
   }
 }
 
@@ -1753,6 +1767,13 @@ extern "C" int vgposp_exact_refine_pending(VGPOSP_EXACT_PARAMS, int batch, const
   VG_CHECK_ARG(picks != nullptr, 25);
   VG_CHECK_ARG(cg_tol >= 0.0, 26);
   const long long* pk = reinterpret_cast<const long long*>(picks);
+  const long long nblk = ceil_div(a.n, EB), nsb = ceil_div(nblk, ESB);
+  {
+    ProfScope ps("exact_stall", s, 0.0, 0.0);
+    hipLaunchKernelGGL(exact_stall_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
+                       nblk, nsb, exact_slots(kmax), batch);
+    VG_LAUNCH_CHECK();
+  }
   return dispatch_kind(kind, [&](auto K) {
     return exact_refine_t<decltype(K)::value>(a, const_cast<double*>(qdiag), cache, selected, w,
                                               batch, w.rf_cand, w.rf_slot, pk, radius, cg_iters,
