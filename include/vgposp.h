@@ -512,7 +512,8 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  *     within K stencil steps, sorted by step count (offset 0 first); tab_cnt int [K + 1]: offsets
  *     within d steps; tab_nb int [T][m - 1]: row of (offset + offsets[o]) in the table or -1.
  *     T <= 1024, T (m - 1) <= 8192.
- *   vgposp_exact_prepare(flags = 1): round 0 from those bounds (cache = upper bounds).
+ *   vgposp_exact_prepare(flags = 1): round 0 from those bounds (cache = upper bounds); flags = 3:
+ *     the same, the bounds being the first of two levels (vgposp_exact_tighten_pending).
  *   vgposp_exact_steps_reset: clears the rounds' control block (after prepare, before the rounds).
  *   vgposp_exact_steps:   rounds [round0, round1) of a run of k picks, decided on the device.
  *     Each round is two kernels: the first refreshes the arg-max keys of the previous round's
@@ -520,14 +521,21 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  *     it (its Q_yy exact, its column in a slot: picks[round] / pick_delta[round], the pick's rows
  *     of chol(Q_AA) and chol(Sigma_AA + jitter I)) or STALLS: the control block records the round
  *     and the refinement
- *     batch (the `batch` <= 32 best entries without a column, each given a free column slot or the
- *     oldest unpinned one); every later kernel of the issued rounds then does nothing.  The second
- *     re-scores the window of the pick (upper bounds where Q_yy is still only bounded).
- *   vgposp_exact_refine_pending: Q e_c for the pending batch by one batched CG (columns into
+ *     batch: every later kernel of the issued rounds then does nothing.  The second re-scores the
+ *     window of the pick (upper bounds where Q_yy is still only bounded).  After the rounds one
+ *     kernel chooses the batch of a stalled round: of the `batch` <= 32 best entries without a
+ *     column, those still on their first (K_lo-step) bound go to the TIGHTENING list, the others
+ *     and the arg-max to the CG batch, each given a free column slot or the oldest unpinned one.
+ *   vgposp_exact_tighten_pending: the tightening list's bounds again with the K_hi-step table
+ *     (arguments as vgposp_exact_bounds; the smaller of the two bounds is kept), the candidates'
+ *     cache entries re-scored; clears the stall when the CG batch is empty.  m = 7 only.
+ *   vgposp_exact_refine_pending: Q e_c for the pending CG batch by one batched CG (columns into
  *     their slots); each Q_cc becomes exact and the candidate's cache entry the reference's value
- *     (scored with the A of its last re-score); clears the stall.
+ *     (scored with the A of its last re-score); clears the stall.  After the tightening when both
+ *     are pending.
  *   vgposp_exact_ctl:     device address of the control block, int32 [8]: stalled round (-1:
- *     none), pending batch size, refined-not-picked count, refinement batches, candidates refined.
+ *     none), CG batch size, refined-not-picked count, refinement batches, candidates refined,
+ *     refinement counter, tightening list size, candidates tightened.
  *   vgposp_exact_update:  after pick `round`: the factor rows and the window re-score (upper
  *     bounds where Q_yy is still only bounded); vgposp_exact_steps issues it per round.
  *   The caller issues rounds, reads the control block, and on a stall refines the pending batch
@@ -559,6 +567,9 @@ int vgposp_exact_steps(VGPOSP_EXACT_ARGS, int round0, int round1, int k, int bat
                        int64_t* picks, double* pick_delta, void* stream);
 int vgposp_exact_refine_pending(VGPOSP_EXACT_ARGS, int batch, const int64_t* picks, double cg_tol,
                                 void* stream);
+int vgposp_exact_tighten_pending(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
+                                 const int* tab_cnt, int T, int K, double hi_scale,
+                                 const int64_t* picks, void* stream);
 int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
                      int cg_iters, int** ctl);
 int vgposp_exact_update(VGPOSP_EXACT_ARGS, int round, const int64_t* picks, void* stream);

@@ -111,6 +111,32 @@ def test_bounded_alg3_matches_oracle(shape, k, cutoff, beta, kind):
     assert g.refine_batches <= 2 * k and k <= g.refinements <= REFINE_BATCH * g.refine_batches
 
 
+@pytest.mark.parametrize("shape,k,cutoff,kind", [
+    ((14, 13, 12), 30, 3, "matern32"),
+    ((20, 16, 14), 40, 2, "eq"),
+])
+def test_two_bound_levels_equal_one(shape, k, cutoff, kind):
+    """The K_lo bounds + tightening to K_hi before a CG column, and one K = 5 level for all: the
+    same picks and pick deltas (bit for bit: every pick's delta comes from its exact Q_yy either
+    way), the oracle's picks."""
+    from vgposp_amd.sparse_placement import ExactTaperPlacement
+    X, ls = _grid(shape, seed=k + 3)
+    out = []
+    for two in (True, False):
+        run = ExactTaperPlacement(X, shape, k, cutoff, 4.0, kind, ls=ls, diag_shift=SHIFT,
+                                  method="bounds")
+        run.greedy.two_level = two
+        A = [int(a) for a in run.run().cpu().numpy()]
+        g = run.greedy
+        assert (g.tight is not None) == two
+        out.append((A, g.pick_delta[:k].cpu().numpy(), g.tightened))
+    assert out[0][0] == out[1][0]
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert out[0][2] > 0 and out[1][2] == 0
+    rA, _, _ = op.placement_window_precision(_dense(X, shape, 4.0, ls, kind), k, shape, cutoff)
+    assert out[0][0] == rA
+
+
 @pytest.mark.parametrize("shape,k,cutoff", [
     ((1, 1, 40), 6, 3),      # a line of candidates
     ((2, 3, 50), 9, 2),
@@ -136,7 +162,8 @@ def test_bounded_edge_cases_match_oracle(shape, k, cutoff):
 ])
 def test_bounds_bracket_dense_inverse(shape, beta, kind):
     """vgposp_exact_bounds: g_K <= Q_yy <= qhi, with qhi within 4 rho^2K (+ margin) of Q_yy."""
-    from vgposp_amd.sparse_placement import ExactWindowGreedy, TaperProblem
+    from vgposp_amd.sparse_placement import (BOUND_HI_TARGET, BOUND_LO_TARGET, ExactWindowGreedy,
+                                             TaperProblem)
     X, ls = _grid(shape, seed=sum(shape) + 1)
     C = _dense(X, shape, beta, ls, kind) + 1e-6 * np.eye(len(X))
     ref = np.diag(np.linalg.inv(C))
@@ -147,7 +174,14 @@ def test_bounds_bracket_dense_inverse(shape, beta, kind):
     hi = q.cpu().numpy()
     assert np.all(hi >= ref)
     assert np.all(hi <= ref * scale * (1 + 1e-13))
-    assert width <= 1e-6
+    assert width <= BOUND_LO_TARGET
+    t = g.tight
+    if t is not None:             # the second level (the K_hi table) brackets too, tighter
+        q3 = torch.zeros_like(q)
+        g.bound_qdiag(q3, steps=t)
+        hi3 = q3.cpu().numpy()
+        assert t[0] > K and t[2] <= BOUND_HI_TARGET
+        assert np.all(hi3 >= ref) and np.all(hi3 <= ref * t[1] * (1 + 1e-13))
     # the same bounds slab by slab
     q2 = torch.zeros_like(q)
     n = prob.n

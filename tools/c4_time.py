@@ -1,7 +1,7 @@
 """C4 (128^3, k = 50, beta 4, cutoff 3) end-to-end run time, as bench.py's c4 line measures it:
-python tools/c4_time.py [--reps R] [batch ...] -> one JSON line per refinement batch size: mean ms
+python tools/c4_time.py [--reps R] [--one-level] [batch ...] -> one JSON line per refinement batch size: mean ms
 over R (10) runs, picks vs tests/golden/c4_picks.json, refinements / batches / host reads, and a profiled run's
-per-phase event times."""
+per-phase event times.  --one-level: one bound level for all candidates (no tightening)."""
 import json
 import os
 import sys
@@ -20,9 +20,12 @@ args = sys.argv[1:]
 REPS = 10
 if args[:1] == ["--reps"]:
     REPS, args = int(args[1]), args[2:]
+ONE = "--one-level" in args
+args = [a for a in args if a != "--one-level"]
 X, shape, ls = c4_grid()
 run = ExactTaperPlacement(X, shape, 50, 3, 4.0, ls=ls, diag_shift=0.01 + 1e-6, method="bounds")
 g = run.greedy
+g.two_level = not ONE
 for B in [int(v) for v in args] or [8]:
     orig = g.run_bounded
     g.run_bounded = lambda q, k, _o=orig, _b=B: _o(q, k, batch=_b)
@@ -42,7 +45,8 @@ for B in [int(v) for v in args] or [8]:
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
     g.run_bounded = orig
-    print(json.dumps({"batch": B, "ms_mean": 1e3 * sum(ts) / len(ts), "ms_min": 1e3 * min(ts),
+    print(json.dumps({"batch": B, "levels": 1 if ONE else 2, "bound": g.bound, "tight": g.tight,
+                      "tightened": g.tightened, "ms_mean": 1e3 * sum(ts) / len(ts), "ms_min": 1e3 * min(ts),
                       "picks_equal": picks == want, "refinements": g.refinements,
                       "batches": g.refine_batches, "host_reads": getattr(g, "host_reads", None),
                       "prof_ms": {k: round(v[0], 3) for k, v in prof.items()},

@@ -23,13 +23,13 @@ F=$(ls $O/pmc_FETCH_SIZE/*counter_collection.csv | head -1)
 W=$(ls $O/pmc_WRITE_SIZE/*counter_collection.csv | head -1)
 python3 $R/tools/pmc_traffic.py $F $W --N 65536 --shape 64 32 32 --k 50 --out $O/traffic_r4.json --command "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-include-regex 'gemm_glds|greedy_trmv|kernel_matrix' -- python3 bench.py $ARGS" > /dev/null
 echo ok traffic
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o c4 -- python3 $R/tools/c4_time.py --reps 1 8 > $O/c4.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o c4 -- python3 $R/tools/c4_time.py --reps 1 32 > $O/c4.log 2>&1
 python3 $R/tools/rocprof_summary.py $O/c4/c4_kernel_stats.csv $O/c4_summary.txt 25 > /dev/null
 echo ok c4 stats
 for c in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   n=$(echo $c | cut -d' ' -f1)
-  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex 'exact_' --output-format csv -d $O/c4pmc_$n -o p -- python3 $R/tools/c4_time.py --reps 1 8 > $O/c4pmc_$n.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex 'exact_' --output-format csv -d $O/c4pmc_$n -o p -- python3 $R/tools/c4_time.py --reps 1 32 > $O/c4pmc_$n.log 2>&1
   echo ok c4 pmc $n
 done
-python3 $R/tools/pmc_c4.py $(ls $O/c4pmc_FETCH_SIZE/*counter_collection.csv | head -1) $(ls $O/c4pmc_WRITE_SIZE/*counter_collection.csv | head -1) $(ls $O/c4pmc_TCC_HIT_sum/*counter_collection.csv | head -1) --runs 3 --out $O/pmc_c4_r4.json --command "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum} --kernel-include-regex exact_ -- python3 tools/c4_time.py --reps 1 8" > $O/pmc_c4.txt
+python3 $R/tools/pmc_c4.py $(ls $O/c4pmc_FETCH_SIZE/*counter_collection.csv | head -1) $(ls $O/c4pmc_WRITE_SIZE/*counter_collection.csv | head -1) $(ls $O/c4pmc_TCC_HIT_sum/*counter_collection.csv | head -1) --runs 3 --out $O/pmc_c4_r4.json --command "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum} --kernel-include-regex exact_ -- python3 tools/c4_time.py --reps 1 32" > $O/pmc_c4.txt
 echo done

@@ -70,7 +70,8 @@ struct ExactWS {
   double* LQ;         // [kmax][kmax] chol(Q_AA)
   double* Qcols;      // [nslots][bv]: Q e_c on candidate c's box (zero outside it)
   int* slot_of_round; // [kmax]: the column slot of pick t
-  unsigned char* qexact;  // [n]: 1 = qdiag[y] is Q_yy, 0 = an upper bound of it
+  unsigned char* qexact;  // [n]: 1 = qdiag[y] is Q_yy; 0 = an upper bound from the K_lo-step
+                          // bounds, 2 = a tightened (K_hi-step) upper bound
   unsigned char* lastA;   // [n]: |A| when y's cache entry was last scored (0: round 0)
   long long* cand;    // [2]: scratch (the arg-max candidate of the round-3 host loop)
   double* gersh;      // [2 + 2 CG_BLOCKS]: lambda_min / lambda_max bounds, then partials
@@ -81,6 +82,7 @@ struct ExactWS {
   unsigned char* rl_pin;  // [nslots]: 1 = the slot is a pick's column (never recycled)
   long long* rf_cand; // [CG_B]: the pending refinement batch (-1: unused column)
   int* rf_slot;       // [CG_B]
+  long long* rt_cand; // [CG_B]: the pending tightening list (ctl[CTL_NT] entries)
   size_t bytes;
 };
 
@@ -91,6 +93,8 @@ constexpr int CTL_UNPICKED = 2;  // refined candidates not (yet) picked
 constexpr int CTL_EVENTS = 3;    // refinement batches in this run
 constexpr int CTL_REFINED = 4;   // candidates refined in this run
 constexpr int CTL_AGE = 5;       // refinement counter (rl_age)
+constexpr int CTL_NT = 6;        // candidates in the pending tightening list (rt_cand)
+constexpr int CTL_TIGHT = 7;     // candidates tightened in this run
 constexpr int CTL_N = 8;
 
 // coefficient rows padded to an even count of doubles (16-byte aligned rows: two-double loads)
@@ -149,6 +153,7 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
   w.rl_pin = (unsigned char*)take((size_t)exact_slots(kmax));
   w.rf_cand = (long long*)take(8 * CG_B);
   w.rf_slot = (int*)take(4 * CG_B);
+  w.rt_cand = (long long*)take(8 * CG_B);
   w.bytes = off;
   return w;
 }
@@ -399,12 +404,13 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
 // coefficients (SM x (M1 + 1) doubles per lane) are loaded into registers once, all loads in
 // flight together, so its K steps run on registers and LDS only (the generic kernel above waits on
 // one coefficient load at a time).  Neighbours outside the table read a zero LDS entry.
-template <int SM, int M1>
+template <int SM, int M1, bool LIST = false>
 __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
     const int* __restrict__ tab_cnt, int T, int K, double hi_scale, long long c0, long long c1,
-    double* __restrict__ qhi) {
+    double* __restrict__ qhi, const long long* __restrict__ list = nullptr,
+    const int* __restrict__ list_count = nullptr) {
   constexpr int TP = SM * 64;
   __shared__ double plds[BND_WAVES][TP + 1];
   __shared__ short nbl[TP * M1];
@@ -424,14 +430,21 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
   // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so XCD x (= blockIdx.x
   // mod 8) walks its own contiguous eighth of the candidates and neighbouring candidates, whose
   // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
+  // LIST: the candidates list[0 .. *list_count) (the tightening of a refinement event)
+  const long long nlist = LIST ? (long long)*list_count : 0;
 #if VGPOSP_BND_RR  // (A/B: the plain round-robin order)
-  for (long long y = c0 + (long long)blockIdx.x * BND_WAVES + wave; y < c1;
-       y += (long long)gridDim.x * BND_WAVES) {
+  for (long long it_y = LIST ? (long long)blockIdx.x * BND_WAVES + wave
+                             : c0 + (long long)blockIdx.x * BND_WAVES + wave;
+       LIST ? it_y < nlist : it_y < c1; it_y += (long long)gridDim.x * BND_WAVES) {
+    const long long y = LIST ? list[it_y] : it_y;
 #else
   const long long per_xcd = (c1 - c0 + 7) / 8, xlo = c0 + (blockIdx.x & 7) * per_xcd;
   const long long xhi = min(c1, xlo + per_xcd);
-  for (long long y = xlo + (long long)(blockIdx.x >> 3) * BND_WAVES + wave; y < xhi;
-       y += (long long)(gridDim.x >> 3) * BND_WAVES) {
+  for (long long it_y = LIST ? (long long)blockIdx.x * BND_WAVES + wave
+                             : xlo + (long long)(blockIdx.x >> 3) * BND_WAVES + wave;
+       LIST ? it_y < nlist : it_y < xhi;
+       it_y += LIST ? (long long)gridDim.x * BND_WAVES : (long long)(gridDim.x >> 3) * BND_WAVES) {
+    const long long y = LIST ? list[it_y] : it_y;
 #endif
     const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
     double c[SM][M];
@@ -502,7 +515,8 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (lane == 0) qhi[y] = g * hi_scale;
+    // (LIST: both bounds are valid, the smaller one is kept)
+    if (lane == 0) qhi[y] = LIST ? fmin(qhi[y], g * hi_scale) : g * hi_scale;
   }
 }
 
@@ -515,7 +529,7 @@ __global__ __launch_bounds__(256) void exact_score_kernel(EArgs a, const double*
   const long long y = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (y >= a.n) return;
   const double nom = sigma_diag<KIND>(a);
-  cache[y] = delta_from(nom, qdiag[y], qexact[y] != 0, a.jitter, a.thr);
+  cache[y] = delta_from(nom, qdiag[y], qexact[y] == 1, a.jitter, a.thr);
 }
 
 // One wave: key of block b (entries [b EB, (b+1) EB) of the cache, selected ones excluded).
@@ -1145,6 +1159,42 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_refine_end_kernel(EArgs a, 
   }
 }
 
+// After the tightening bounds of a refinement event (the K_hi-step bounds of rt_cand): each
+// candidate's cache entry is re-scored from its tighter upper bound with the A of its last re-score,
+// its keys refreshed; the stall is cleared unless CG columns are pending too (their
+// exact_refine_end_kernel clears it).  One workgroup.
+template <int KIND>
+__global__ __launch_bounds__(SEL_THREADS) void exact_tighten_end_kernel(EArgs a, const double* qdiag,
+                                                                        double* cache,
+                                                                        unsigned char* sel,
+                                                                        ExactWS w, long long nblk,
+                                                                        const long long* picks) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int NWAVE = SEL_THREADS / 64;
+  const int nt = w.ctl[CTL_NT];
+  for (int j = wave; j < nt; j += NWAVE) {
+    const long long c = w.rt_cand[j];
+    const double d = wave_rescore<KIND>(a, w, global_rows(w, a.kmax), picks, (int)w.lastA[c], c,
+                                        qdiag[c], false);
+    if (lane == 0) {
+      w.qexact[c] = 2;
+      cache[c] = d;
+    }
+  }
+  __syncthreads();
+  for (int j = wave; j < nt; j += NWAVE)
+    wave_block_key(cache, sel, a.n, w.rt_cand[j] / EB, w.bval, w.bidx);
+  __syncthreads();
+  for (int j = wave; j < nt; j += NWAVE)
+    wave_super_key(w.bval, w.bidx, nblk, w.rt_cand[j] / EB / ESB, w.sval, w.sidx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    w.ctl[CTL_TIGHT] += nt;
+    w.ctl[CTL_NT] = 0;
+    if (w.ctl[CTL_NB] == 0) w.ctl[CTL_STALL] = -1;
+  }
+}
+
 // After q_t = Q e_{a_t}, part 1: row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I) (one wave
 // each; the earlier rows staged in LDS when they fit, the right-hand sides computed by all lanes
 // at once, then one forward substitution with lane s holding z_s).
@@ -1237,7 +1287,7 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
     if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
     return;
   }
-  const double d = wave_rescore<KIND>(a, w, L, picks, round + 1, y, qdiag[y], w.qexact[y] != 0);
+  const double d = wave_rescore<KIND>(a, w, L, picks, round + 1, y, qdiag[y], w.qexact[y] == 1);
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
@@ -1397,11 +1447,22 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
   }
   __syncthreads();
   if (t == 0) {
+    // without a column: a candidate still on its K_lo bound is tightened (K_hi bound, cheap); one
+    // already tightened (or exact but recycled), and the arg-max itself, gets its CG column (the
+    // arg-max would stall the next event on its own otherwise)
     long long* todo = s_todo;
-    int nt = 0;
-    for (int b = 0; b < ntop; ++b)
-      if (!s_has[b]) todo[nt++] = top[1 + b];
-    if (nt == 0) todo[nt++] = a;
+    int nt = 0, ntight = 0;
+    for (int b = 0; b < ntop; ++b) {
+      if (s_has[b]) continue;
+      const long long y = top[1 + b];
+      if (w.qexact[y] == 0 && y != a) w.rt_cand[ntight++] = y;
+      else todo[nt++] = y;
+    }
+    if (nt == 0 && ntight == 0) {
+      if (w.qexact[a] == 0) w.rt_cand[ntight++] = a;
+      else todo[nt++] = a;
+    }
+    w.ctl[CTL_NT] = ntight;
     const int nfree = s_nfree, nold = s_nold;
     int nb = 0, age = w.ctl[CTL_AGE], recycled = 0;
     for (int j = 0; j < nt; ++j) {
@@ -1495,7 +1556,8 @@ int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned
   const bool bounded = (flags & 1) != 0;
   VG_HIP(vg_memset(sel, 0, n, s));
   VG_HIP(vg_memset(w.lastA, 0, n, s));
-  VG_HIP(vg_memset(w.qexact, bounded ? 0 : 1, n, s));
+  // 0: on the K_lo bound, to be tightened first (flags & 2: a second bound level); 2: final bound
+  VG_HIP(vg_memset(w.qexact, bounded ? ((flags & 2) ? 0 : 2) : 1, n, s));
   if (!bounded) {
     hipLaunchKernelGGL(exact_coef_kernel<KIND>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
                        a, w.coef);
@@ -1641,7 +1703,7 @@ extern "C" size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I
 
 extern "C" int vgposp_exact_prepare(VGPOSP_EXACT_PARAMS, int flags, void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_prepare");
-  VG_CHECK_ARG(flags == 0 || flags == 1, 24);
+  VG_CHECK_ARG(flags == 0 || flags == 1 || flags == 3, 24);
   return dispatch_kind(kind, [&](auto K) {
     return exact_prepare_t<decltype(K)::value>(a, qdiag, cache, selected, w, flags, s);
   });
@@ -1756,6 +1818,12 @@ extern "C" int vgposp_exact_steps(VGPOSP_EXACT_PARAMS, int round0, int round1, i
         VG_LAUNCH_CHECK();
       }
     }
+    // if a round stalled: choose its batch now, so ONE read of the control block tells the host
+    // what to run (no-op otherwise)
+    ProfScope ps("exact_stall", s, 0.0, 0.0);
+    hipLaunchKernelGGL(exact_stall_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
+                       nblk, nsb, exact_slots(kmax), batch);
+    VG_LAUNCH_CHECK();
     return 0;
   });
 }
@@ -1767,13 +1835,6 @@ extern "C" int vgposp_exact_refine_pending(VGPOSP_EXACT_PARAMS, int batch, const
   VG_CHECK_ARG(picks != nullptr, 25);
   VG_CHECK_ARG(cg_tol >= 0.0, 26);
   const long long* pk = reinterpret_cast<const long long*>(picks);
-  const long long nblk = ceil_div(a.n, EB), nsb = ceil_div(nblk, ESB);
-  {
-    ProfScope ps("exact_stall", s, 0.0, 0.0);
-    hipLaunchKernelGGL(exact_stall_kernel, dim3(1), dim3(SEL_THREADS), 0, s, cache, selected, a.n, w,
-                       nblk, nsb, exact_slots(kmax), batch);
-    VG_LAUNCH_CHECK();
-  }
   return dispatch_kind(kind, [&](auto K) {
     return exact_refine_t<decltype(K)::value>(a, const_cast<double*>(qdiag), cache, selected, w,
                                               batch, w.rf_cand, w.rf_slot, pk, radius, cg_iters,
@@ -1806,6 +1867,43 @@ extern "C" int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2
   if (cand) *cand = reinterpret_cast<int64_t*>(w.cand);
   if (gersh) *gersh = w.gersh;
   return 0;
+}
+
+extern "C" int vgposp_exact_tighten_pending(VGPOSP_EXACT_PARAMS, const int* tab_off,
+                                            const int* tab_nb, const int* tab_cnt, int T, int K,
+                                            double hi_scale, const int64_t* picks, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_tighten_pending");
+  VG_CHECK_ARG(tab_off != nullptr && tab_nb != nullptr && tab_cnt != nullptr, 24);
+  VG_CHECK_ARG(T >= 1 && T <= BND_TMAX && (int64_t)T * (m - 1) <= BND_NBMAX, 27);
+  VG_CHECK_ARG(K >= 1 && K <= 4 * BND_SMAX, 28);
+  VG_CHECK_ARG(hi_scale >= 1.0, 29);
+  VG_CHECK_ARG(picks != nullptr, 30);
+  VG_CHECK_ARG(a.m1 == 6, 12);  // the register bounds kernel (the 7-point taper)
+  const long long nblk = ceil_div(a.n, EB);
+  double* out = const_cast<double*>(qdiag);
+  const unsigned blocks = (unsigned)ceil_div(CG_B, BND_WAVES);
+  {
+    ProfScope ps("exact_tighten", s, 0.0, 0.0);
+#define VG_TIGHT_REG(SMV)                                                                        \
+  if (T <= 64 * SMV) {                                                                           \
+    hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6, true>), dim3(blocks), dim3(BND_T), 0, s,   \
+                       w.coef, a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, 0LL,   \
+                       0LL, out, w.rt_cand, w.ctl + CTL_NT);                                      \
+  } else
+    VG_TIGHT_REG(4) VG_TIGHT_REG(6) VG_TIGHT_REG(9) VG_TIGHT_REG(14) {
+      set_error("vgposp_exact_tighten_pending: reach table of %d nodes", T);
+      return 27;
+    }
+#undef VG_TIGHT_REG
+    VG_LAUNCH_CHECK();
+  }
+  return dispatch_kind(kind, [&](auto KK) {
+    hipLaunchKernelGGL(exact_tighten_end_kernel<decltype(KK)::value>, dim3(1), dim3(SEL_THREADS), 0, s,
+                       a, qdiag, cache, selected, w, nblk,
+                       reinterpret_cast<const long long*>(picks));
+    VG_LAUNCH_CHECK();
+    return 0;
+  });
 }
 
 extern "C" int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax,

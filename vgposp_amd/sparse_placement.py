@@ -411,6 +411,12 @@ REFINE_BATCH = 32       # candidates refined together by one batched CG (vgposp_
 #                         measured at 128^3: batch 8 14.3 ms, 16 13.4, 32 12.4 (profiles/r4_c4_batch_*)
 REFINE_BATCH_MAX = 32   # the library's CG_B
 BOUND_MARGIN = 1e-12                       # relative rounding margin on the upper bounds
+# Two-level bounds: every candidate gets the K_lo-step bound (bracket width <= BOUND_LO_TARGET:
+# K = 4 at the reference's beta = 4), the few that reach a refinement batch the K_hi-step one
+# (width <= BOUND_HI_TARGET, K = 6) before any of them is given a CG column.  One K = 5 level for
+# all (round 3's) cost the 2M-candidate bounds pass 4.8 ms at 128^3.
+BOUND_LO_TARGET = 3e-5
+BOUND_HI_TARGET = 1e-7
 
 
 def bound_steps(offsets, lam_min, lam_max, target=1e-6, kmax=12):
@@ -464,6 +470,9 @@ class ExactWindowGreedy:
         self.refinements = 0      # candidates refined (CG columns) in the last bounded run
         self.refine_batches = 0   # batched CG solves in the last bounded run
         self.bound = None
+        self.tight = None
+        self.two_level = True     # bound_qdiag's default: two bound levels (7-point stencils)
+        self.tightened = 0        # candidates tightened to the K_hi bound in the last bounded run
 
     def _args(self, qdiag):
         pr = self.p
@@ -497,15 +506,29 @@ class ExactWindowGreedy:
         g = self.ws[off: off + 16].view(torch.float64).cpu()
         return float(g[0]), float(g[1])
 
-    def bound_qdiag(self, qdiag, c0=0, c1=None, steps=None):
+    def bound_qdiag(self, qdiag, c0=0, c1=None, steps=None, tighten=None):
         """qdiag[c0:c1] <- upper bounds of Q_yy (vgposp_exact_bounds).  Returns the (K, hi_scale,
         width) used, or None when the spectrum bounds cannot bracket Q_yy (then the selected
-        inverse is the only exact route)."""
+        inverse is the only exact route).  With ``tighten`` (7-point stencils) the bounds are
+        the K_lo-step ones and run_bounded tightens candidates to K_hi steps before their CG
+        column (``self.tight`` = the K_hi triple, None when there is no second level; default
+        ``self.two_level``)."""
+        tighten = self.two_level if tighten is None else tighten
         lo, hi = self.gershgorin(qdiag)
-        b = bound_steps(self.p.offs_np, lo, hi) if steps is None else steps
+        offs = self.p.offs_np
+        two = tighten and steps is None and len(offs.reshape(-1, 3)) == 6
+        if steps is not None:
+            b = steps
+        else:
+            b = bound_steps(offs, lo, hi, target=BOUND_LO_TARGET if two else 1e-6)
         self.bound = b
+        self.tight = None
         if b is None:
             return None
+        if two:
+            t = bound_steps(offs, lo, hi, target=BOUND_HI_TARGET)
+            if t is not None and t[0] > b[0]:
+                self.tight = t
         # the measured spectrum bounds are tighter than the kernel-agnostic one the columns were
         # sized with: fewer CG iterations (and a smaller Krylov box) give the same tolerance
         its = cg_iterations_for(lo, hi, self.cg_tol)
@@ -513,17 +536,23 @@ class ExactWindowGreedy:
             self.cg_iters = its
             self.box = [min(2 * self.radius * its + 1, s) for s in self.p.shape]
         K, scale, _ = b
-        if getattr(self, "_tabK", None) != K:   # the reach tables, uploaded once per K
+        tab, T = self._device_table(K)
+        c1 = self.p.n if c1 is None else int(c1)
+        call("vgposp_exact_bounds", *self._args(qdiag), *[_p(a) for a in tab], T, K, scale,
+             int(c0), c1, _stream())
+        return b
+
+    def _device_table(self, K):
+        """The reach table of K steps on the device (int32: offsets, neighbours, counts), uploaded
+        once per K."""
+        tabs = self.__dict__.setdefault("_tabs", {})
+        if K not in tabs:
             tab, cnt, nb = reach_table(self.p.offs_np, K)
             dev = self.p.device
-            self._tab = [torch.as_tensor(np.ascontiguousarray(a).reshape(-1), dtype=torch.int32,
-                                         device=dev) for a in (tab, nb if nb.size else np.zeros(1),
-                                                               cnt)]
-            self._tabK, self._T = K, len(tab)
-        c1 = self.p.n if c1 is None else int(c1)
-        call("vgposp_exact_bounds", *self._args(qdiag), _p(self._tab[0]), _p(self._tab[1]),
-             _p(self._tab[2]), self._T, K, scale, int(c0), c1, _stream())
-        return b
+            tabs[K] = ([torch.as_tensor(np.ascontiguousarray(a).reshape(-1), dtype=torch.int32,
+                                        device=dev)
+                        for a in (tab, nb if nb.size else np.zeros(1), cnt)], len(tab))
+        return tabs[K]
 
     def run_bounded(self, qdiag, k, batch=None):
         """The rounds with qdiag holding upper bounds of Q_yy: the cache holds upper bounds of the
@@ -548,18 +577,28 @@ class ExactWindowGreedy:
         self.picks.fill_(-1)
         args = self._args(qdiag)
         st = _stream()
-        call("vgposp_exact_prepare", *args, 1, st)
+        tight = self.tight
+        call("vgposp_exact_prepare", *args, 1 if tight is None else 3, st)
         call("vgposp_exact_steps_reset", *args, st)
         ctl = self._ctl()
         pk, pd = _p(self.picks), _p(self.pick_delta)
+        if tight is not None:
+            ttab, tT = self._device_table(tight[0])
+            targs = (*[_p(a) for a in ttab], tT, tight[0], tight[1], pk)
         call("vgposp_exact_steps", *args, 0, 1, k, B, pk, pd, st)  # round 0 stalls: nothing refined
         issued, reads = 1, 0
         while True:
-            c = ctl.cpu().tolist()  # stall round, batch size, refined-unpicked, events, refined
+            # stall round, CG batch, refined-unpicked, events, refined, age, tightening list, tightened
+            c = ctl.cpu().tolist()
             reads += 1
             stall = c[0]
             if stall >= 0:
-                call("vgposp_exact_refine_pending", *args, B, pk, self.cg_tol, st)
+                if c[6] > 0:
+                    if tight is None:
+                        raise RuntimeError("tightening list without a K_hi table")
+                    call("vgposp_exact_tighten_pending", *args, *targs, st)
+                if c[1] > 0:
+                    call("vgposp_exact_refine_pending", *args, B, pk, self.cg_tol, st)
                 r0, r1 = stall, min(k, stall + c[2] + c[1] + 1)
             elif issued < k:
                 r0, r1 = issued, min(k, issued + max(c[2], 0) + 1)
@@ -568,6 +607,7 @@ class ExactWindowGreedy:
             call("vgposp_exact_steps", *args, r0, r1, k, B, pk, pd, st)
             issued = r1
         self.refinements, self.refine_batches, self.host_reads = c[4], c[3], reads
+        self.tightened = c[7]
         return self.picks[:k]
 
     def _ctl(self):
