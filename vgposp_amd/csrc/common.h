@@ -54,11 +54,85 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---- device helpers -------------------------------------------------------------------------
 
-// Wave64 reductions.
+// Wave64 butterfly reductions without the LDS crossbar.  Every reduction here is the descending
+// xor butterfly (partner lane i ^ o for o = 32, 16, 8, 4, 2, 1; at each step a lane combines its
+// value with its partner's), computed with cross-lane VALU ops instead of ds_bpermute (__shfl_xor
+// is one LDS-crossbar round trip per 32-bit word per step, and the latency-bound C4 kernels spent
+// most of their time in those chains):
+//   o = 32, 16: v_permlane32_swap / v_permlane16_swap (CDNA4) with both operands the value, which
+//               returns the two halves' (rows') values {own half, other half} in a fixed order;
+//   o = 8:      DPP row_ror:8 (rotating a 16-lane row by 8 is lane i ^ 8 exactly);
+//   o = 4:      DPP row_ror:4, which is lane i ^ 4 whenever lanes i and i ^ 8 hold the same value —
+//               always true after the o = 8 step of a descending butterfly;
+//   o = 2, 1:   DPP quad_perm [2,3,0,1] / [1,0,3,2].
+// The combining operators used with it (+, min, max, the key arg-max) are commutative, so the
+// results are bit-identical to the __shfl_xor butterfly they replace.  Whole waves only.
+template <int O>
+__device__ __forceinline__ void xor_pair32(unsigned x, unsigned& a, unsigned& b) {
+  if constexpr (O == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    a = r[0];
+    b = r[1];
+  } else if constexpr (O == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    a = r[0];
+    b = r[1];
+  } else {
+    constexpr int CTRL = O == 8 ? 0x128 : O == 4 ? 0x124 : O == 2 ? 0x4E : 0xB1;
+    static_assert(O == 8 || O == 4 || O == 2 || O == 1, "butterfly step");
+    a = x;
+    b = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+  }
+}
+
+// The two values of a butterfly step for a 64-bit word: {a, b} = {own, partner} (o <= 8) or
+// {lower half / even row, upper half / odd row} (o = 32 / 16); either way the step's result is
+// op(a, b) for a commutative op.
+template <int O, class T>
+__device__ __forceinline__ void xor_pair64(T v, T& a, T& b) {
+  static_assert(sizeof(T) == 8, "64-bit words");
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  unsigned a0, b0, a1, b1;
+  xor_pair32<O>((unsigned)u, a0, b0);
+  xor_pair32<O>((unsigned)(u >> 32), a1, b1);
+  a = __builtin_bit_cast(T, (unsigned long long)a0 | ((unsigned long long)a1 << 32));
+  b = __builtin_bit_cast(T, (unsigned long long)b0 | ((unsigned long long)b1 << 32));
+}
+
+template <int O, class Op>
+__device__ __forceinline__ double wave_step(double v, Op op) {
+  double a, b;
+  xor_pair64<O>(v, a, b);
+  return op(a, b);
+}
+
+// Every lane returns op over the wave's 64 values (op commutative).
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op) {
+  v = wave_step<32>(v, op);
+  v = wave_step<16>(v, op);
+  v = wave_step<8>(v, op);
+  v = wave_step<4>(v, op);
+  v = wave_step<2>(v, op);
+  return wave_step<1>(v, op);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](double a, double b) { return a + b; });
+}
+__device__ __forceinline__ double wave_min(double v) {
+  return wave_reduce(v, [](double a, double b) { return fmin(a, b); });
+}
+__device__ __forceinline__ double wave_max(double v) {
+  return wave_reduce(v, [](double a, double b) { return fmax(a, b); });
+}
+
+// Lane `src`'s value (src wave-uniform), as a uniform value.
+__device__ __forceinline__ double wave_bcast(double v, int src) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), src);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
 }
 
 // (value, index) arg-max with the reference's tie rule: larger value wins; on equal value the
@@ -79,17 +153,28 @@ __device__ __forceinline__ bool key_gt(double v1, long long i1, double v2, long 
   return (v1 > v2) || (v1 == v2 && i1 < i2);
 }
 
-__device__ __forceinline__ void wave_keymax(double& v, long long& i) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    double ov = __shfl_xor(v, o, 64);
-    long long oi = __shfl_xor(i, o, 64);
-    if (key_gt(ov, oi, v, i)) {
-      v = ov;
-      i = oi;
-    }
-  }
+template <int O>
+__device__ __forceinline__ void wave_keystep(double& v, long long& i) {
+  double va, vb;
+  long long ia, ib;
+  xor_pair64<O>(v, va, vb);
+  xor_pair64<O>(i, ia, ib);
+  const bool b_wins = key_gt(vb, ib, va, ia);
+  v = b_wins ? vb : va;
+  i = b_wins ? ib : ia;
 }
+
+// Every lane returns the wave's key arg-max (the butterfly of wave_reduce; key_gt is a strict
+// total order, so the result does not depend on the pairing).
+__device__ __forceinline__ void wave_keymax(double& v, long long& i) {
+  wave_keystep<32>(v, i);
+  wave_keystep<16>(v, i);
+  wave_keystep<8>(v, i);
+  wave_keystep<4>(v, i);
+  wave_keystep<2>(v, i);
+  wave_keystep<1>(v, i);
+}
+
 
 }  // namespace vgposp
 

@@ -255,11 +255,8 @@ __global__ __launch_bounds__(256) void exact_gersh_kernel(const double* __restri
     lo = fmin(lo, c[0] - s);
     hi = fmax(hi, c[0] + s);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
-  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
   if ((threadIdx.x & 63) == 0) {
     rl[threadIdx.x >> 6] = lo;
     rh[threadIdx.x >> 6] = hi;
@@ -277,11 +274,8 @@ __global__ __launch_bounds__(64) void exact_gersh_final_kernel(double* part, int
     lo = fmin(lo, part[2 + i]);
     hi = fmax(hi, part[2 + CG_BLOCKS + i]);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
-  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
   if (threadIdx.x == 0) {
     part[0] = lo;
     part[1] = hi;
@@ -404,8 +398,16 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
 // coefficients (SM x (M1 + 1) doubles per lane) are loaded into registers once, all loads in
 // flight together, so its K steps run on registers and LDS only (the generic kernel above waits on
 // one coefficient load at a time).  Neighbours outside the table read a zero LDS entry.
+#ifndef VGPOSP_BND_WPE  // (A/B: waves per SIMD the register allocation must allow; 0 = default)
+#define VGPOSP_BND_WPE 0
+#endif
+#if VGPOSP_BND_WPE
+#define VG_BND_ATTR __attribute__((amdgpu_waves_per_eu(VGPOSP_BND_WPE)))
+#else
+#define VG_BND_ATTR
+#endif
 template <int SM, int M1, bool LIST = false>
-__global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
+__global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
     const int* __restrict__ tab_cnt, int T, int K, double hi_scale, long long c0, long long c1,
@@ -427,6 +429,20 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
   if (lane == 0) pl[TP] = 0.0;
   __syncthreads();
   constexpr int M = M1 + 1;
+  // the lane's neighbour byte offsets into pl, two per register: the reach table is relative, so
+  // they are the same for every candidate and every step (read from LDS once, not once per gather)
+  constexpr int NP = (M1 + 1) / 2;
+  unsigned nbo[SM][NP];
+#pragma unroll
+  for (int s = 0; s < SM; ++s)
+#pragma unroll
+    for (int o = 0; o < NP; ++o) {
+      const int j = s * 64 + lane;
+      const unsigned lo = 8u * (unsigned)nbl[j * M1 + 2 * o];
+      const unsigned hi = 2 * o + 1 < M1 ? 8u * (unsigned)nbl[j * M1 + 2 * o + 1] : 0u;
+      nbo[s][o] = lo | (hi << 16);
+    }
+  const char* plb = reinterpret_cast<const char*>(pl);
   // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so XCD x (= blockIdx.x
   // mod 8) walks its own contiguous eighth of the candidates and neighbouring candidates, whose
   // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
@@ -485,7 +501,10 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
           const int j = s * 64 + lane;
           double acc = c[s][0] * p[s];
 #pragma unroll
-          for (int o = 0; o < M1; ++o) acc = fma(c[s][1 + o], pl[nbl[j * M1 + o]], acc);
+          for (int o = 0; o < M1; ++o) {
+            const unsigned off = (nbo[s][o >> 1] >> (16 * (o & 1))) & 0xffffu;
+            acc = fma(c[s][1 + o], *reinterpret_cast<const double*>(plb + off), acc);
+          }
           q[s] = j < cnt ? acc : 0.0;
           pq = fma(p[s], q[s], pq);
         }
@@ -1038,6 +1057,29 @@ __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int n
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
 constexpr int EX_SLOTS_MAX = 2 * EX_KMAX;  // column slots (exact_slots(kmax) <= this)
 
+// (A/B builds only, -DVGPOSP_EXACT_DBG=1: thread 0 of the per-round kernels stamps its phases with
+// the 100 MHz real-time counter; vgposp_exact_dbg copies the last 64 records out.)
+#ifndef VGPOSP_EXACT_DBG
+#define VGPOSP_EXACT_DBG 0
+#endif
+#if VGPOSP_EXACT_DBG
+__device__ unsigned long long g_exact_dbg[64][8];
+__device__ unsigned int g_exact_dbg_n;
+#define DBG_DECL unsigned long long dbg_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define DBG_T(k) \
+  if (threadIdx.x == 0) dbg_t[k] = __builtin_amdgcn_s_memrealtime();
+#define DBG_END(kind)                                                         \
+  if (threadIdx.x == 0) {                                                     \
+    dbg_t[7] = (kind);                                                        \
+    const unsigned slot = atomicAdd(&g_exact_dbg_n, 1u) & 63u;                \
+    for (int q = 0; q < 8; ++q) g_exact_dbg[slot][q] = dbg_t[q];              \
+  }
+#else
+#define DBG_DECL
+#define DBG_T(k)
+#define DBG_END(kind)
+#endif
+
 // Rows of chol(Q_AA) / chol(S_AA + eps I): in the workspace (row stride kmax) or packed lower
 // triangles staged in LDS (row r at r (r + 1) / 2).
 struct FactorRows {
@@ -1069,22 +1111,105 @@ __device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int km, int n
   return FactorRows{sm, sm + np, 0};
 }
 
+// What a re-score needs of pick r, staged in LDS once per workgroup: its grid coordinates and
+// point, and where its CG column lives (box origin, element offset of its slot).  Read straight
+// from the workspace, sigma_off / qcol_at cost three to four DEPENDENT global loads per lane
+// (picks -> X, slot_of_round -> boxlo -> Qcols) on the critical path of every round.
+struct StagedPicks {
+  int g[EX_KMAX][3];
+  double x[EX_KMAX][3];
+  long long lo[EX_KMAX][3];
+  long long base[EX_KMAX];
+};
+
+// Picks 0 .. nA-1 (the whole workgroup calls it; the caller synchronises before use).
+__device__ __forceinline__ void stage_picks(const EArgs& a, const ExactWS& w,
+                                            const long long* picks, int nA, StagedPicks& sp) {
+  const long long bv = w.b0 * w.b1 * w.b2;
+  for (int r = threadIdx.x; r < nA; r += blockDim.x) {
+    const long long i = picks[r];
+    const int slot = w.slot_of_round[r];
+    sp.g[r][0] = (int)(i / (a.I1 * a.I2));
+    sp.g[r][1] = (int)((i / a.I2) % a.I1);
+    sp.g[r][2] = (int)(i % a.I2);
+    sp.x[r][0] = a.X[3 * i];
+    sp.x[r][1] = a.X[3 * i + 1];
+    sp.x[r][2] = a.X[3 * i + 2];
+    sp.lo[r][0] = w.boxlo[3 * slot];
+    sp.lo[r][1] = w.boxlo[3 * slot + 1];
+    sp.lo[r][2] = w.boxlo[3 * slot + 2];
+    sp.base[r] = (long long)slot * bv;
+  }
+}
+
+// A candidate (grid coordinates c, point xy) as the re-score sees it.
+struct CandPoint {
+  long long c0, c1, c2;
+  double x0, x1, x2;
+};
+
+__device__ __forceinline__ CandPoint cand_point(const EArgs& a, long long y) {
+  CandPoint c;
+  c.c0 = y / (a.I1 * a.I2);
+  c.c1 = (y / a.I2) % a.I1;
+  c.c2 = y % a.I2;
+  c.x0 = a.X[3 * y];
+  c.x1 = a.X[3 * y + 1];
+  c.x2 = a.X[3 * y + 2];
+  return c;
+}
+
+// sigma_off(a, pick r, y) from the staged pick: the same operations in the same order, so the
+// same bits.
+template <int KIND>
+__device__ __forceinline__ double sigma_off_staged(const EArgs& a, const StagedPicks& sp, int r,
+                                                   const CandPoint& c) {
+  const long long e0 = sp.g[r][0] - c.c0, e1 = sp.g[r][1] - c.c1, e2 = sp.g[r][2] - c.c2;
+  const long long d2i = e0 * e0 + e1 * e1 + e2 * e2;
+  if (d2i >= a.ntau) return 0.0;
+  const double t = a.tau[d2i];
+  if (t == 0.0) return 0.0;
+  const double d0 = sp.x[r][0] - c.x0, d1 = sp.x[r][1] - c.x1, d2 = sp.x[r][2] - c.x2;
+  return t * kfun<KIND>(d0 * d0 + d1 * d1 + d2 * d2, a.tla, a.inv_ls, a.inv_ls2);
+}
+
+// qcol_at(w, r, y) from the staged pick.
+__device__ __forceinline__ double qcol_staged(const ExactWS& w, const StagedPicks& sp, int r,
+                                              const CandPoint& c) {
+  const long long l0 = c.c0 - sp.lo[r][0], l1 = c.c1 - sp.lo[r][1], l2 = c.c2 - sp.lo[r][2];
+  if (l0 < 0 || l0 >= w.b0 || l1 < 0 || l1 >= w.b1 || l2 < 0 || l2 >= w.b2) return 0.0;
+  return w.Qcols[sp.base[r] + (l0 * w.b1 + l1) * w.b2 + l2];
+}
+
 // The cached delta of candidate y given the first nA picks, one wave: nominator
 // s_yy - |LS^-1 s_Ay|^2, P = qyy - |LQ^-1 q_Ay|^2.  Lane s holds the forward-substitution
-// unknowns z_s and z_{s+64}; every lane returns the delta.
+// unknowns z_s and z_{s+64}; every lane returns the delta.  sp: the picks staged in LDS
+// (stage_picks) or nullptr (read from the workspace).
 template <int KIND>
 __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRows& L,
                                const long long* picks, int nA, long long y, double qyy,
-                               bool exact) {
+                               bool exact, const StagedPicks* sp = nullptr) {
   const int lane = threadIdx.x & 63;
   double vs0 = 0.0, vq0 = 0.0, vs1 = 0.0, vq1 = 0.0;
-  if (lane < nA) {
-    vs0 = sigma_off<KIND>(a, picks[lane], y);
-    vq0 = qcol_at(w, lane, y, a.I1, a.I2);
-  }
-  if (lane + 64 < nA) {
-    vs1 = sigma_off<KIND>(a, picks[lane + 64], y);
-    vq1 = qcol_at(w, lane + 64, y, a.I1, a.I2);
+  if (sp) {
+    const CandPoint c = cand_point(a, y);
+    if (lane < nA) {
+      vs0 = sigma_off_staged<KIND>(a, *sp, lane, c);
+      vq0 = qcol_staged(w, *sp, lane, c);
+    }
+    if (lane + 64 < nA) {
+      vs1 = sigma_off_staged<KIND>(a, *sp, lane + 64, c);
+      vq1 = qcol_staged(w, *sp, lane + 64, c);
+    }
+  } else {
+    if (lane < nA) {
+      vs0 = sigma_off<KIND>(a, picks[lane], y);
+      vq0 = qcol_at(w, lane, y, a.I1, a.I2);
+    }
+    if (lane + 64 < nA) {
+      vs1 = sigma_off<KIND>(a, picks[lane + 64], y);
+      vq1 = qcol_at(w, lane + 64, y, a.I1, a.I2);
+    }
   }
   double zs0 = 0.0, zq0 = 0.0, zs1 = 0.0, zq1 = 0.0;
   for (int r = 0; r < nA; ++r) {
@@ -1209,13 +1334,17 @@ __device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
   const int km = a.kmax;
   const long long at = picks[round];
   if (at < 0) return;
+  __shared__ StagedPicks sp;
+  stage_picks(a, w, picks, round + 1, sp);
   const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, km, round, sm)
-                                                        : global_rows(w, km);
+                                                        : (__syncthreads(), global_rows(w, km));
   if (wave > 1) return;
   const double* Lm = wave == 0 ? L.lq : L.ls;
+  // (the staged forms of qcol_at(w, round, picks[r]) and sigma_off(a, at, picks[r]))
   auto val = [&](int r) {
-    if (wave == 0) return qcol_at(w, round, picks[r], a.I1, a.I2);
-    return r == round ? sigma_diag<KIND>(a) + a.jitter : sigma_off<KIND>(a, at, picks[r]);
+    const CandPoint c{sp.g[r][0], sp.g[r][1], sp.g[r][2], sp.x[r][0], sp.x[r][1], sp.x[r][2]};
+    if (wave == 0) return qcol_staged(w, sp, round, c);
+    return r == round ? sigma_diag<KIND>(a) + a.jitter : sigma_off_staged<KIND>(a, sp, round, c);
   };
   const double v0 = lane <= round ? val(lane) : 0.0;
   const double v1 = lane + 64 <= round ? val(lane + 64) : 0.0;
@@ -1237,7 +1366,7 @@ __device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
   if (lane < round) Lw[lane] = z0;
   if (lane + 64 < round) Lw[lane + 64] = z1;
   // diagonal: sqrt(v_round - |z|^2), v_round held by lane round % 64
-  const double vr = __shfl(round < 64 ? v0 : v1, round & 63, 64);
+  const double vr = wave_bcast(round < 64 ? v0 : v1, round & 63);
   if (lane == 0) Lw[round] = sqrt(vr - nz);
 }
 
@@ -1272,13 +1401,15 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
                                                            ExactWS w, int round,
                                                            const long long* picks) {
   __shared__ double sm[ROWS_LDS];
+  __shared__ StagedPicks sp;
   const long long at = picks[round];
   if (at < 0) return;
   const Window v = window_of(a, at);
-  // every candidate of the workgroup walks the same factor rows: stage them once
+  // every candidate of the workgroup walks the same factor rows and picks: stage them once
   const int nr = round + 1;
+  stage_picks(a, w, picks, nr, sp);
   const FactorRows L = nr * (nr + 1) <= ROWS_LDS ? stage_rows(w, a.kmax, nr, sm)
-                                                 : global_rows(w, a.kmax);
+                                                 : (__syncthreads(), global_rows(w, a.kmax));
   const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= v.w0 * v.w1 * v.w2) return;
   const long long y = ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) * a.I2 +
@@ -1287,7 +1418,8 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
     if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
     return;
   }
-  const double d = wave_rescore<KIND>(a, w, L, picks, round + 1, y, qdiag[y], w.qexact[y] == 1);
+  const double d = wave_rescore<KIND>(a, w, L, picks, round + 1, y, qdiag[y], w.qexact[y] == 1,
+                                      &sp);
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
@@ -1361,17 +1493,22 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
                                                                  double* pick_delta) {
   __shared__ int s_slot;
   __shared__ double sm[ROWS_LDS];
+  DBG_DECL
+  DBG_T(0)
   if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
   const long long n = ea.n;
   if (round > 0 && picks[round - 1] >= 0)
     block_window_keys(ea, cache, sel, w, nblk, picks[round - 1]);
+  DBG_T(1)
   const long long a = block_argmax(w, nsb);
+  DBG_T(2)
   if (threadIdx.x == 0) s_slot = -1;
   __syncthreads();
   if (a >= 0)
     for (int i = threadIdx.x; i < nslots; i += SEL_THREADS)
       if (w.rl_cand[i] == a) s_slot = i;
   __syncthreads();
+  DBG_T(3)
   const int slot = s_slot;
   if (a < 0 || slot >= 0) {  // pick (no candidate left: picks[round] = -1, nothing changes)
     if (threadIdx.x == 0) {
@@ -1387,7 +1524,10 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
     }
     __syncthreads();
     if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
+    DBG_T(4)
     if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm);
+    DBG_T(5)
+    DBG_END(2)
     return;
   }
   // stall: the batch is chosen by exact_stall_kernel, which the host launches first thing in
@@ -1404,28 +1544,38 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
                                                                   int nslots, int B) {
   __shared__ long long top[CG_B + 1];
   __shared__ long long s_todo[CG_B];
+  DBG_DECL
+  DBG_T(0)
   if (w.ctl[CTL_STALL] < 0) return;
   const long long a = block_argmax(w, nsb);
+  DBG_T(1)
   // stall: the B best entries without a column become the refinement batch.  The slot table is
   // staged in LDS and ranked in parallel (a first version walked it with thread 0's dependent
   // global loads: 750 us per stall at B = 32): free slots are taken first, lowest index first,
   // then the unpinned ones, oldest refinement first — the candidates in the batch have no column,
   // so no slot of theirs can be recycled.
   block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
+  DBG_T(2)
   __shared__ long long s_cand[EX_SLOTS_MAX];
   __shared__ int s_age[EX_SLOTS_MAX], s_inv_free[EX_SLOTS_MAX], s_inv_old[EX_SLOTS_MAX];
   __shared__ unsigned char s_pin[EX_SLOTS_MAX];
   __shared__ int s_has[CG_B], s_nfree, s_nold;
+  __shared__ unsigned char s_qx[CG_B + 1];  // qexact of the top entries and of the arg-max
   const int t = threadIdx.x;
+  const int ntop = (int)top[0];
   if (t < nslots) {
     s_cand[t] = w.rl_cand[t];
     s_age[t] = w.rl_age[t];
     s_pin[t] = w.rl_pin[t];
   }
   if (t < CG_B) s_has[t] = 0;
+  // (loaded in parallel here: thread 0's serial loop below would otherwise wait on one dependent
+  // byte load per entry — its stores may alias them)
+  if (t < ntop) s_qx[t] = w.qexact[top[1 + t]];
+  if (t == CG_B && a >= 0) s_qx[CG_B] = w.qexact[a];
   if (t == 0) s_nfree = s_nold = 0;
   __syncthreads();
-  const int ntop = (int)top[0];
+  DBG_T(3)
   for (int e = t; e < nslots * ntop; e += SEL_THREADS) {
     const int i = e / ntop, b = e % ntop;
     if (s_cand[i] >= 0 && s_cand[i] == top[1 + b]) s_has[b] = 1;
@@ -1446,6 +1596,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
     }
   }
   __syncthreads();
+  DBG_T(4)
   if (t == 0) {
     // without a column: a candidate still on its K_lo bound is tightened (K_hi bound, cheap); one
     // already tightened (or exact but recycled), and the arg-max itself, gets its CG column (the
@@ -1455,11 +1606,11 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
     for (int b = 0; b < ntop; ++b) {
       if (s_has[b]) continue;
       const long long y = top[1 + b];
-      if (w.qexact[y] == 0 && y != a) w.rt_cand[ntight++] = y;
+      if (s_qx[b] == 0 && y != a) w.rt_cand[ntight++] = y;
       else todo[nt++] = y;
     }
     if (nt == 0 && ntight == 0) {
-      if (w.qexact[a] == 0) w.rt_cand[ntight++] = a;
+      if (s_qx[CG_B] == 0) w.rt_cand[ntight++] = a;
       else todo[nt++] = a;
     }
     w.ctl[CTL_NT] = ntight;
@@ -1489,6 +1640,8 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
     w.ctl[CTL_UNPICKED] -= recycled;
     w.ctl[CTL_NB] = nb;
   }
+  DBG_T(5)
+  DBG_END(1)
 }
 
 }  // namespace vgposp
@@ -1694,6 +1847,15 @@ int exact_refine_t(const EArgs& a, double* qdiag, double* cache, unsigned char* 
   const EArgs a = make_eargs(X, I0, I1, I2, amp, ls, diag_shift, jitter, threshold, offsets, m, \
                              tau, ntau, kmax, cutoff);                                           \
   hipStream_t s = as_stream(stream)
+
+#if VGPOSP_EXACT_DBG
+extern "C" int vgposp_exact_dbg(unsigned long long* out) {  // 64 x 8 records, then reset
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(vgposp::g_exact_dbg), sizeof(vgposp::g_exact_dbg));
+  const unsigned z = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(vgposp::g_exact_dbg_n), &z, sizeof(z));
+  return 0;
+}
+#endif
 
 extern "C" size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
                                                int radius, int cg_iters) {

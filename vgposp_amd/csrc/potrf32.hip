@@ -167,7 +167,7 @@ __global__ void refine_phi_kernel(double* E, int64_t n, unsigned long long* amax
     mx = fmax(mx, fabs(e));
     E[r * n + c] = c < r ? e : (c == r ? 0.5 * e : 0.0);
   }
-  for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+  mx = wave_max(mx);
   if ((threadIdx.x & 63) == 0) atomicMax(amax, (unsigned long long)__double_as_longlong(mx));
 }
 
