@@ -354,8 +354,8 @@ def c4_line(args, world, rank, barrier, maxtime):
     """Config C4: 128^3 = 2,097,152 candidates, k = 50, the reference's algorithm 3
     (snippets_a3.py:43-364) on the beta = 4 tapered covariance, window cutoff 3, exact
     (vgposp_amd.sparse_placement).  One step = the bounded-lazy form end to end: stencil
-    coefficients, upper bounds of every Q_yy from 8 CG steps per candidate (sharded over the
-    ranks, one all-gather), then the k rounds (refining a candidate by its CG column whenever the
+    coefficients, upper bounds of every Q_yy from K CG steps per candidate (Gauss-Radau bounds,
+    K = 4 at beta = 4; sharded over the ranks, one all-gather), then the k rounds (refining a candidate by its CG column whenever the
     arg-max lands on a bounded one; replicated on every rank).  The multifrontal selected inverse
     (exact diag(Q) on fp64 MFMA fronts, subtree-to-subcube over the ranks) runs once beside it as
     the cross-check of the picks and reports its own rate."""
@@ -421,6 +421,8 @@ def c4_line(args, world, rank, barrier, maxtime):
            "matches_committed_picks": (_committed("c4_picks.json", picks)
                                        if k == 50 and args.noise == 1e-2 else None),
            "bounds": {"ms": bounds_ms, "cg_steps": K, "bracket_rel_width": width,
+                      "form": "gauss-radau" if g.bound_mu > 0 else "chebyshev",
+                      "mu": g.bound_mu,
                       "candidates_this_rank": nb,
                       "mcandidates_per_s": nb / (bounds_ms * 1e-3) / 1e6},
            "allgather_ms": gather_ms if world > 1 else None,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define VGPOSP_ABI_VERSION 1
+#define VGPOSP_ABI_VERSION 2
 
 #define VGPOSP_E_HIP (-100)
 #define VGPOSP_E_WS (-101)
@@ -506,9 +506,11 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  * Bounded-lazy form (no selected inverse; same picks):
  *   vgposp_exact_coef:    the stencil coefficients and Gershgorin bounds [lambda_min, lambda_max]
  *     of Sigma + jitter I (device doubles, vgposp_exact_buffers' `gersh`).
- *   vgposp_exact_bounds:  qdiag[y] for y in [c0, c1) <- hi_scale * g_K(y), g_K = the K-step CG
- *     estimate of e_y^T (Sigma + jitter I)^-1 e_y from x = 0 (a lower bound; hi_scale =
- *     (1 + margin) / (1 - 4 rho^2K) makes it an upper bound).  tab_off int [T][3]: the offsets
+ *   vgposp_exact_bounds:  qdiag[y] for y in [c0, c1) <- an upper bound of e_y^T (Sigma + jitter I)^-1
+ *     e_y from K CG steps from x = 0: with mu = 0, hi_scale * g_K (g_K = the CG estimate, a
+ *     lower bound; hi_scale = (1 + margin) / (1 - 4 rho^2K)); with 0 < mu <= lambda_min, the
+ *     Gauss-Radau bound hi_scale * (g_K + gamma^mu_K |r_K|^2) (hi_scale = 1 + margin; the
+ *     recurrence is in exact_greedy.hip).  tab_off int [T][3]: the offsets
  *     within K stencil steps, sorted by step count (offset 0 first); tab_cnt int [K + 1]: offsets
  *     within d steps; tab_nb int [T][m - 1]: row of (offset + offsets[o]) in the table or -1.
  *     T <= 1024, T (m - 1) <= 8192.
@@ -560,15 +562,15 @@ int vgposp_exact_round(VGPOSP_EXACT_ARGS, int round, int last, int64_t* picks, d
                        double cg_tol, void* stream);
 int vgposp_exact_coef(VGPOSP_EXACT_ARGS, void* stream);
 int vgposp_exact_bounds(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
-                        const int* tab_cnt, int T, int K, double hi_scale, int64_t c0, int64_t c1,
-                        void* stream);
+                        const int* tab_cnt, int T, int K, double hi_scale, double mu, int64_t c0,
+                        int64_t c1, void* stream);
 int vgposp_exact_steps_reset(VGPOSP_EXACT_ARGS, void* stream);
 int vgposp_exact_steps(VGPOSP_EXACT_ARGS, int round0, int round1, int k, int batch,
                        int64_t* picks, double* pick_delta, void* stream);
 int vgposp_exact_refine_pending(VGPOSP_EXACT_ARGS, int batch, const int64_t* picks, double cg_tol,
                                 void* stream);
 int vgposp_exact_tighten_pending(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
-                                 const int* tab_cnt, int T, int K, double hi_scale,
+                                 const int* tab_cnt, int T, int K, double hi_scale, double mu,
                                  const int64_t* picks, void* stream);
 int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
                      int cg_iters, int** ctl);

@@ -53,9 +53,10 @@ def _gershgorin(Ce):
     return float((np.diag(Ce) - off).min()), float((np.diag(Ce) + off).max())
 
 
-def _cg_bounds(Ce, shape, offs, K, scale):
+def _cg_bounds(Ce, shape, offs, K, scale, mu=0.0):
     """exact_bounds_kernel restated: K CG steps from e_y on the reach-table nodes around y
-    (clipped to the grid), g = sum alpha_i |r_i|^2, upper bound scale * g."""
+    (clipped to the grid), g = sum alpha_i |r_i|^2, upper bound scale * g (mu = 0) or the
+    Gauss-Radau bound scale * (g + gamma^mu_K |r_K|^2) (0 < mu <= lambda_min)."""
     tab, cnt, nb = reach_table(offs, K)
     I0, I1, I2 = shape
     out = np.zeros(len(Ce))
@@ -68,16 +69,19 @@ def _cg_bounds(Ce, shape, offs, K, scale):
         r = np.zeros(len(idx))
         r[0] = 1.0
         p = r.copy()
-        rr, acc = 1.0, 0.0
+        rr, acc, gmu = 1.0, 0.0, (1.0 / mu if mu > 0 else 0.0)
         for _ in range(K):
             q = A @ p
             alpha = rr / (p @ q)
             acc += alpha * rr
             r = r - alpha * q
             rn = r @ r
+            if mu > 0:
+                d = gmu - alpha
+                gmu = d / (mu * d + rn / rr)
             p = r + (rn / rr) * p
             rr = rn
-        out[y] = scale * acc
+        out[y] = scale * (acc + gmu * rr) if mu > 0 else scale * acc
     return out
 
 
@@ -94,6 +98,26 @@ def test_cg_bounds_bracket_q(shape, kind):
         _, scale, _ = bound_steps(offs, lo, hi, kmax=K)
         qhi = _cg_bounds(Ce, shape, offs, K, scale)
         assert np.all(qhi >= Q)
+
+
+@pytest.mark.parametrize("shape,kind", [((6, 7, 8), "eq"), ((5, 9, 4), "matern32")])
+def test_radau_bounds_bracket_q(shape, kind):
+    """The Gauss-Radau upper bound (mu = the Gershgorin lambda_min) holds at every K and after K
+    steps brackets Q_yy at least as tightly as the Chebyshev bound after K (on the beta = 4 taper,
+    about as tightly as Chebyshev after K + 1: sparse_placement.radau_steps)."""
+    C, Ce = _problem(shape, kind=kind)
+    offs, _ = taper_support(4.0)
+    Q = np.diag(np.linalg.inv(Ce))
+    lo, hi = _gershgorin(Ce)
+    assert 0 < lo <= np.linalg.eigvalsh(Ce)[0]
+    for K in (1, 2, 3, 4, 5):
+        _, cscale, cwidth = bound_steps(offs, lo, hi, kmax=K)
+        rad = _cg_bounds(Ce, shape, offs, K, 1.0 + 1e-12, mu=lo)
+        cheb = _cg_bounds(Ce, shape, offs, K, cscale)
+        assert np.all(rad >= Q), K
+        assert np.all(rad <= cheb * (1 + 1e-13)), K
+        _, _, wnext = bound_steps(offs, lo, hi, kmax=K + 1)
+        assert (rad / Q - 1).max() <= 4 * wnext, (K, (rad / Q - 1).max(), wnext)
 
 
 def _delta_ub(nom, P, exact):

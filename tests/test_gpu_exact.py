@@ -160,8 +160,11 @@ def test_bounded_edge_cases_match_oracle(shape, k, cutoff):
     ((9, 10, 11), 4.0, "matern52"),
     ((3, 4, 30), 4.0, "matern12"),
 ])
-def test_bounds_bracket_dense_inverse(shape, beta, kind):
-    """vgposp_exact_bounds: g_K <= Q_yy <= qhi, with qhi within 4 rho^2K (+ margin) of Q_yy."""
+@pytest.mark.parametrize("radau", [True, False])
+def test_bounds_bracket_dense_inverse(shape, beta, kind, radau):
+    """vgposp_exact_bounds: g_K <= Q_yy <= qhi; Chebyshev (mu = 0): qhi within 4 rho^2K (+ margin)
+    of Q_yy; Gauss-Radau (mu = the Gershgorin lambda_min, one step fewer): within 4x the
+    Chebyshev width of K + 1 steps, and the second level's bounds tighter."""
     from vgposp_amd.sparse_placement import (BOUND_HI_TARGET, BOUND_LO_TARGET, ExactWindowGreedy,
                                              TaperProblem)
     X, ls = _grid(shape, seed=sum(shape) + 1)
@@ -169,19 +172,29 @@ def test_bounds_bracket_dense_inverse(shape, beta, kind):
     ref = np.diag(np.linalg.inv(C))
     prob = TaperProblem(X, shape, beta, kind, ls=ls, diag_shift=SHIFT)
     g = ExactWindowGreedy(prob, 4, 3)
+    g.radau = radau
     q = torch.zeros(prob.n, dtype=torch.float64, device="cuda")
     K, scale, width = g.bound_qdiag(q)
     hi = q.cpu().numpy()
     assert np.all(hi >= ref)
-    assert np.all(hi <= ref * scale * (1 + 1e-13))
+    if radau:
+        assert g.bound_mu > 0 and scale == 1.0 + 1e-12
+        assert np.all(hi <= ref * (1 + 4 * width))
+    else:
+        assert g.bound_mu == 0.0
+        assert np.all(hi <= ref * scale * (1 + 1e-13))
     assert width <= BOUND_LO_TARGET
     t = g.tight
     if t is not None:             # the second level (the K_hi table) brackets too, tighter
         q3 = torch.zeros_like(q)
-        g.bound_qdiag(q3, steps=t)
+        g.bound_qdiag(q3, steps=t, mu=g.bound_mu)
         hi3 = q3.cpu().numpy()
         assert t[0] > K and t[2] <= BOUND_HI_TARGET
-        assert np.all(hi3 >= ref) and np.all(hi3 <= ref * t[1] * (1 + 1e-13))
+        assert np.all(hi3 >= ref)
+        if radau:
+            assert np.all(hi3 <= ref * (1 + 4 * t[2]))
+        else:
+            assert np.all(hi3 <= ref * t[1] * (1 + 1e-13))
     # the same bounds slab by slab
     q2 = torch.zeros_like(q)
     n = prob.n

@@ -1,5 +1,6 @@
 """GPU: the library's cross-lane wave reductions (csrc/common.h — DPP row rotates / quad perms and
-v_permlane32/16_swap) return bit for bit what the __shfl_xor butterflies they replaced returned,
+v_permlane32/16_swap; the key arg-max on an order-preserving integer encoding) return bit for bit
+what the __shfl_xor / key_gt butterflies they replaced returned,
 on values chosen to make the summation order visible (mixed magnitudes and signs), ties in the key
 arg-max, NaN keys and missing (-1) indices.  The checker kernel is tests/hip/wave_check.hip."""
 import ctypes
@@ -34,10 +35,12 @@ def test_wave_reductions_bit_identical_to_shuffle_butterfly():
     bits = o.view(np.uint64)
     for new, old in ((0, 1), (2, 3), (4, 5), (6, 7)):
         same = bits[..., new] == bits[..., old]
-        if new < 4:  # a sum / min over a NaN is NaN either way; its payload bits are not compared
-            same |= np.isnan(o[..., new]) & np.isnan(o[..., old])
-        if new == 4:  # with no candidate (index -1) the value carries nothing (callers pass 0.0)
-            same |= o[..., 7].view(np.int64) < 0
+        # a NaN is NaN either way (its payload bits are not compared); the key arg-max returns
+        # -0.0 as +0.0 (key_gt ranks them equal)
+        same |= np.isnan(o[..., new]) & np.isnan(o[..., old])
+        if new == 4:
+            same |= o[..., 4] == o[..., 5]
+            same |= o[..., 7].view(np.int64) < 0  # no candidate: the value carries nothing
         bad = np.argwhere(~same)
         assert bad.size == 0, (new, bad[:8].tolist(), o[tuple(bad[0])][[new, old]])
     # and the values are the reductions (every lane holds the same result)

@@ -1,5 +1,5 @@
 """C4 (128^3, k = 50, beta 4, cutoff 3) end-to-end run time, as bench.py's c4 line measures it:
-python tools/c4_time.py [--reps R] [--one-level] [batch ...] -> one JSON line per refinement batch size: mean ms
+python tools/c4_time.py [--reps R] [--two-level] [--cheb] [batch ...] -> one JSON line per refinement batch size: mean ms
 over R (10) runs, picks vs tests/golden/c4_picks.json, refinements / batches / host reads, and a profiled run's
 per-phase event times.  --one-level: one bound level for all candidates (no tightening)."""
 import json
@@ -20,12 +20,14 @@ args = sys.argv[1:]
 REPS = 10
 if args[:1] == ["--reps"]:
     REPS, args = int(args[1]), args[2:]
-ONE = "--one-level" in args
-args = [a for a in args if a != "--one-level"]
+ONE = "--two-level" not in args  # (the default is one bound level)
+CHEB = "--cheb" in args  # the Chebyshev bounds (K + 1 steps) instead of Gauss-Radau
+args = [a for a in args if a not in ("--one-level", "--two-level", "--cheb")]
 X, shape, ls = c4_grid()
 run = ExactTaperPlacement(X, shape, 50, 3, 4.0, ls=ls, diag_shift=0.01 + 1e-6, method="bounds")
 g = run.greedy
 g.two_level = not ONE
+g.radau = not CHEB
 for B in [int(v) for v in args] or [8]:
     orig = g.run_bounded
     g.run_bounded = lambda q, k, _o=orig, _b=B: _o(q, k, batch=_b)
@@ -45,7 +47,7 @@ for B in [int(v) for v in args] or [8]:
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
     g.run_bounded = orig
-    print(json.dumps({"batch": B, "levels": 1 if ONE else 2, "bound": g.bound, "tight": g.tight,
+    print(json.dumps({"batch": B, "levels": 1 if ONE else 2, "radau": g.radau, "bound": g.bound, "tight": g.tight,
                       "tightened": g.tightened, "ms_mean": 1e3 * sum(ts) / len(ts), "ms_min": 1e3 * min(ts),
                       "picks_equal": picks == want, "refinements": g.refinements,
                       "batches": g.refine_batches, "host_reads": getattr(g, "host_reads", None),

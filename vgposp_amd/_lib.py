@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VGPOSP_LIB", os.path.join(_HERE, "libvgposp.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "vgposp.h")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 E_HIP = -100
 E_WS = -101
 
@@ -140,13 +140,13 @@ SIGNATURES = {
     "vgposp_exact_round": (_i32, _EXACT + [_i32, _i32, _c_void_p, _c_void_p, _f64, _c_void_p]),
     "vgposp_exact_coef": (_i32, _EXACT + [_c_void_p]),
     "vgposp_exact_bounds": (_i32, _EXACT + [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _f64,
-                                            _i64, _i64, _c_void_p]),
+                                            _f64, _i64, _i64, _c_void_p]),
     "vgposp_exact_steps_reset": (_i32, _EXACT + [_c_void_p]),
     "vgposp_exact_steps": (_i32, _EXACT + [_i32, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                            _c_void_p]),
     "vgposp_exact_refine_pending": (_i32, _EXACT + [_i32, _c_void_p, _f64, _c_void_p]),
     "vgposp_exact_tighten_pending": (_i32, _EXACT + [_c_void_p, _c_void_p, _c_void_p, _i32, _i32,
-                                                     _f64, _c_void_p, _c_void_p]),
+                                                     _f64, _f64, _c_void_p, _c_void_p]),
     "vgposp_exact_ctl": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                                 ctypes.POINTER(_c_void_p)]),
     "vgposp_exact_update": (_i32, _EXACT + [_i32, _c_void_p, _c_void_p]),

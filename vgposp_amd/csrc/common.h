@@ -153,26 +153,72 @@ __device__ __forceinline__ bool key_gt(double v1, long long i1, double v2, long 
   return (v1 > v2) || (v1 == v2 && i1 < i2);
 }
 
-template <int O>
-__device__ __forceinline__ void wave_keystep(double& v, long long& i) {
-  double va, vb;
-  long long ia, ib;
-  xor_pair64<O>(v, va, vb);
-  xor_pair64<O>(i, ia, ib);
-  const bool b_wins = key_gt(vb, ib, va, ia);
-  v = b_wins ? vb : va;
-  i = b_wins ? ib : ia;
+// The same order as two unsigned 64-bit words compared lexicographically, so a comparison is
+// three integer compares and no branches: v = an order-preserving code of the value (numbers
+// >= 2, NaN 1, "no candidate" (index < 0) 0; -0 is taken as +0, which key_gt treats as equal to
+// it anyway), i = ~index (a lower index is a larger code; ~(-1) = 0).
+struct Key {
+  unsigned long long v, i;
+};
+
+__device__ __forceinline__ Key key_enc(double v, long long i) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v + 0.0);
+  const unsigned long long o = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  Key k;
+  k.i = ~(unsigned long long)i;
+  k.v = i < 0 ? 0ull : (__builtin_isnan(v) ? 1ull : o);
+  return k;
 }
 
-// Every lane returns the wave's key arg-max (the butterfly of wave_reduce; key_gt is a strict
-// total order, so the result does not depend on the pairing).
+// The value back (0.0 for no candidate, a quiet NaN for NaN).
+__device__ __forceinline__ double key_value(const Key& k) {
+  if (k.v <= 1ull) return k.v ? __builtin_nan("") : 0.0;
+  const unsigned long long u = (k.v >> 63) ? (k.v & 0x7fffffffffffffffull) : ~k.v;
+  return __builtin_bit_cast(double, u);
+}
+
+__device__ __forceinline__ long long key_index(const Key& k) { return (long long)~k.i; }
+
+__device__ __forceinline__ bool key_enc_gt(const Key& a, const Key& b) {
+  return a.v > b.v || (a.v == b.v && a.i > b.i);
+}
+
+// k <- c if c > k (component-wise selects: a select of the whole struct can be lowered through
+// scratch memory with a dynamic index)
+__device__ __forceinline__ void key_take_max(Key& k, const Key& c) {
+  const bool g = key_enc_gt(c, k);
+  k.v = g ? c.v : k.v;
+  k.i = g ? c.i : k.i;
+}
+
+template <int O>
+__device__ __forceinline__ void wave_keystep(Key& k) {
+  Key a, b;
+  xor_pair64<O>(k.v, a.v, b.v);
+  xor_pair64<O>(k.i, a.i, b.i);
+  key_take_max(a, b);
+  k = a;
+}
+
+// Every lane returns the wave's key maximum (the butterfly of wave_reduce; the order is a strict
+// total order on candidates, so the result does not depend on the pairing).
+__device__ __forceinline__ Key wave_keymax(Key k) {
+  wave_keystep<32>(k);
+  wave_keystep<16>(k);
+  wave_keystep<8>(k);
+  wave_keystep<4>(k);
+  wave_keystep<2>(k);
+  wave_keystep<1>(k);
+  return k;
+}
+
+// (value, index) form: every lane returns the wave's arg-max under key_gt (its value as stored,
+// except that -0.0 comes back as +0.0 and a NaN as the quiet NaN; with no candidate, index -1 and
+// value 0.0).
 __device__ __forceinline__ void wave_keymax(double& v, long long& i) {
-  wave_keystep<32>(v, i);
-  wave_keystep<16>(v, i);
-  wave_keystep<8>(v, i);
-  wave_keystep<4>(v, i);
-  wave_keystep<2>(v, i);
-  wave_keystep<1>(v, i);
+  const Key k = wave_keymax(key_enc(v, i));
+  v = key_value(k);
+  i = key_index(k);
 }
 
 

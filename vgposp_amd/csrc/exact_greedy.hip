@@ -45,6 +45,11 @@ constexpr int EB = 256;      // cache entries per block key
 constexpr int ESB = 64;      // blocks per superblock key
 constexpr int CG_BLOCKS = 1024;
 constexpr int CG_T = 256;
+#ifndef VGPOSP_CG_SEG  // (A/B: lanes per diamond row of the 7-point CG walk; 64 = one row per wave)
+#define VGPOSP_CG_SEG 16
+#endif
+constexpr int CG_SEG = VGPOSP_CG_SEG;
+constexpr int CG_RPW = 64 / CG_SEG;  // diamond rows per wave
 constexpr int SEL_THREADS = 1024;
 
 struct ExactWS {
@@ -291,6 +296,28 @@ __global__ __launch_bounds__(64) void exact_gersh_final_kernel(double* part, int
 #ifndef VGPOSP_BND_RR
 #define VGPOSP_BND_RR 0
 #endif
+// Upper bounds of Q_yy = e_y^T (S + eps I)^-1 e_y from K CG steps on (S + eps I) x = e_y, x0 = 0.
+// The CG estimate g_K = sum_k gamma_k |r_k|^2 (gamma_k = alpha_k) is the Gauss-quadrature LOWER
+// bound, and Q_yy - g_K = |x - x_K|_A^2.  Two upper bounds:
+//  * mu = 0: g_K / (1 - 4 rho^2K) (hi_scale carries the factor): the Chebyshev bound on the CG
+//    error, rho from the spectrum bounds;
+//  * mu > 0 (0 < mu <= lambda_min, the Gershgorin lower bound): the Gauss-Radau bound
+//    |x - x_K|_A^2 <= gamma^mu_K |r_K|^2 with gamma^mu_0 = 1 / mu and
+//    gamma^mu_{k+1} = (gamma^mu_k - gamma_k) / (mu (gamma^mu_k - gamma_k) + delta_{k+1}),
+//    delta_{k+1} = |r_{k+1}|^2 / |r_k|^2 (Golub & Meurant, "Matrices, Moments and Quadrature";
+//    the CG form of Meurant & Tichy, Numer. Algorithms 2013, algorithm CGQ); hi_scale is then only
+//    the rounding margin.  On the beta = 4 taper its bracket after K steps is about the Chebyshev
+//    one after K + 1 (9e-7 at K = 4 against 8.5e-7 at K = 5): one CG step fewer per candidate.
+__device__ __forceinline__ double radau_step(double gmu, double gamma, double mu, double delta) {
+  const double d = gmu - gamma;
+  return d / fma(mu, d, delta);
+}
+
+__device__ __forceinline__ double bound_value(double g, double gmu, double rrK, double mu,
+                                              double hi_scale) {
+  return mu > 0.0 ? hi_scale * fma(gmu, rrK, g) : hi_scale * g;
+}
+
 constexpr int BND_T = 256;
 constexpr int BND_WAVES = BND_T / 64;
 constexpr int BND_SMAX = 14;
@@ -300,8 +327,8 @@ constexpr int BND_NBMAX = 8192;
 __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2, int m1,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
-    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, long long c0, long long c1,
-    double* __restrict__ qhi) {
+    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, double mu, long long c0,
+    long long c1, double* __restrict__ qhi) {
   __shared__ double plds[BND_WAVES][BND_TMAX];
   __shared__ short nbl[BND_NBMAX];
   __shared__ short offl[3 * BND_TMAX];
@@ -344,7 +371,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double rr = 1.0, g = 0.0;
+    double rr = 1.0, g = 0.0, gmu = mu > 0.0 ? 1.0 / mu : 0.0;
     for (int it = 0; it < K; ++it) {
       const int cnt = cntl[it + 1];
       double pq = 0.0;
@@ -367,7 +394,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
       pq = wave_sum(pq);
       const double alpha = rr / pq;
       g = fma(alpha, rr, g);
-      if (it + 1 == K) break;
+      if (it + 1 == K && mu <= 0.0) break;
       double rn = 0.0;
 #pragma unroll
       for (int s = 0; s < BND_SMAX; ++s) {
@@ -375,8 +402,10 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
         rn = fma(r[s], r[s], rn);
       }
       rn = wave_sum(rn);
+      if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, rn / rr);
       const double beta = rn / rr;
       rr = rn;
+      if (it + 1 == K) break;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -390,7 +419,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (lane == 0) qhi[y] = g * hi_scale;
+    if (lane == 0) qhi[y] = bound_value(g, gmu, rr, mu, hi_scale);
   }
 }
 
@@ -410,8 +439,8 @@ template <int SM, int M1, bool LIST = false>
 __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
-    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, long long c0, long long c1,
-    double* __restrict__ qhi, const long long* __restrict__ list = nullptr,
+    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, double mu, long long c0,
+    long long c1, double* __restrict__ qhi, const long long* __restrict__ list = nullptr,
     const int* __restrict__ list_count = nullptr) {
   constexpr int TP = SM * 64;
   __shared__ double plds[BND_WAVES][TP + 1];
@@ -490,7 +519,7 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double rr = 1.0, g = 0.0;
+    double rr = 1.0, g = 0.0, gmu = mu > 0.0 ? 1.0 / mu : 0.0;
     for (int it = 0; it < K; ++it) {
       const int cnt = cntl[it + 1];
       double pq = 0.0;
@@ -512,7 +541,7 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
       pq = wave_sum(pq);
       const double alpha = rr / pq;
       g = fma(alpha, rr, g);
-      if (it + 1 == K) break;
+      if (it + 1 == K && mu <= 0.0) break;
       double rn = 0.0;
 #pragma unroll
       for (int s = 0; s < SM; ++s) {
@@ -520,8 +549,10 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
         rn = fma(r[s], r[s], rn);
       }
       rn = wave_sum(rn);
+      if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, rn / rr);
       const double beta = rn / rr;
       rr = rn;
+      if (it + 1 == K) break;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -535,7 +566,8 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // (LIST: both bounds are valid, the smaller one is kept)
-    if (lane == 0) qhi[y] = LIST ? fmin(qhi[y], g * hi_scale) : g * hi_scale;
+    const double ub = bound_value(g, gmu, rr, mu, hi_scale);
+    if (lane == 0) qhi[y] = LIST ? fmin(qhi[y], ub) : ub;
   }
 }
 
@@ -556,22 +588,52 @@ __device__ __forceinline__ void wave_block_key(const double* cache, const unsign
                                                long long n, long long b, double* bval,
                                                long long* bidx) {
   const int lane = threadIdx.x & 63;
-  double v = 0.0;
-  long long idx = -1;
+  Key k{0ull, 0ull};
+#pragma unroll
   for (int e = lane; e < EB; e += 64) {
     const long long y = b * EB + e;
     if (y < n && !sel[y]) {
-      const double c = cache[y];
-      if (key_gt(c, y, v, idx)) {
-        v = c;
-        idx = y;
-      }
+      key_take_max(k, key_enc(cache[y], y));
     }
   }
-  wave_keymax(v, idx);
+  k = wave_keymax(k);
   if (lane == 0) {
-    bval[b] = v;
-    bidx[b] = idx;
+    bval[b] = key_value(k);
+    bidx[b] = key_index(k);
+  }
+}
+
+// Up to NB blocks blk[q] (q < nb) at once, one wave: every block's entries are loaded before any
+// key is reduced or stored, so the blocks' load latencies overlap.
+template <int NB>
+__device__ __forceinline__ void wave_block_keys(const double* cache, const unsigned char* sel,
+                                                long long n, const long long* blk, int nb,
+                                                double* bval, long long* bidx) {
+  const int lane = threadIdx.x & 63;
+  constexpr int PER = EB / 64;
+  double c[NB][PER];
+  unsigned char sl[NB][PER];
+#pragma unroll
+  for (int q = 0; q < NB; ++q)
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const long long y = q < nb ? blk[q] * EB + e * 64 + lane : n;
+      c[q][e] = y < n ? cache[y] : 0.0;
+      sl[q][e] = y < n ? sel[y] : 1;
+    }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    if (q >= nb) break;
+    Key k{0ull, 0ull};
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      key_take_max(k, key_enc(c[q][e], sl[q][e] ? -1 : blk[q] * EB + e * 64 + lane));
+    }
+    k = wave_keymax(k);
+    if (lane == 0) {
+      bval[blk[q]] = key_value(k);
+      bidx[blk[q]] = key_index(k);
+    }
   }
 }
 
@@ -832,17 +894,19 @@ __device__ __forceinline__ void cg_walk(const ExactWS& w, const ActiveCube& q, l
   }
   const long long R = min((long long)it + 1, w.H);
   const long long a0 = a / (I1 * I2), a1 = (a / I2) % I1, a2 = a % I2;
-  const int lane = threadIdx.x & 63;
+  // CG_SEG lanes per diamond row (a row holds 2h + 1 <= 2R + 1 nodes, ~R/2 on average: one row
+  // per wave left most lanes idle and quadrupled the waves of the late iterations)
+  const int lane = threadIdx.x & 63, sub = lane / CG_SEG, sl = lane % CG_SEG;
   const long long nrows = diamond_rows(R);
-  for (long long rw = (long long)blockIdx.x * (CG_T / 64) + (threadIdx.x >> 6); rw < nrows;
-       rw += (long long)gridDim.x * (CG_T / 64)) {
+  for (long long rw = ((long long)blockIdx.x * (CG_T / 64) + (threadIdx.x >> 6)) * CG_RPW + sub;
+       rw < nrows; rw += (long long)gridDim.x * (CG_T / 64) * CG_RPW) {
     long long d0, d1;
     diamond_row(rw, d0, d1);
     const long long g0 = a0 + d0, g1 = a1 + d1;
     if (g0 < 0 || g0 >= I0 || g1 < 0 || g1 >= I1) continue;
     const long long h = R - (d0 < 0 ? -d0 : d0) - (d1 < 0 ? -d1 : d1);
     const long long lo2 = max(a2 - h, 0LL), hi2 = min(a2 + h, I2 - 1);
-    for (long long g2 = lo2 + lane; g2 <= hi2; g2 += 64) f(g0, g1, g2);
+    for (long long g2 = lo2 + sl; g2 <= hi2; g2 += CG_SEG) f(g0, g1, g2);
   }
 }
 
@@ -936,24 +1000,31 @@ template <int P>
 __device__ __forceinline__ void wave_topb(double (&v)[P], long long (&id)[P], int B, double* ov,
                                           long long* oi) {
   const int lane = threadIdx.x & 63;
+  // the branch-free encoded order, held as two plain arrays and selected component-wise (an
+  // array of Key structs selected as a whole went through scratch memory: 540 us per stall)
+  unsigned long long kv[P], ki[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const Key e = key_enc(v[p], id[p]);
+    kv[p] = e.v;
+    ki[p] = e.i;
+  }
   for (int b = 0; b < B; ++b) {
-    double bv = 0.0;
-    long long bi = -1;
+    Key best{kv[0], ki[0]};
 #pragma unroll
-    for (int p = 0; p < P; ++p)
-      if (key_gt(v[p], id[p], bv, bi)) {
-        bv = v[p];
-        bi = id[p];
-      }
-    wave_keymax(bv, bi);
+    for (int p = 1; p < P; ++p) key_take_max(best, Key{kv[p], ki[p]});
+    best = wave_keymax(best);
     if (lane == 0) {
-      ov[b] = bv;
-      oi[b] = bi;
+      ov[b] = key_value(best);
+      oi[b] = key_index(best);
     }
-    if (bi < 0) continue;  // fewer than B items: the rest stay -1
+    if (best.v == 0ull) continue;  // fewer than B items: the rest stay -1
 #pragma unroll
-    for (int p = 0; p < P; ++p)
-      if (id[p] == bi) id[p] = -1;
+    for (int p = 0; p < P; ++p) {
+      const bool hit = ki[p] == best.i;
+      kv[p] = hit ? 0ull : kv[p];
+      ki[p] = hit ? 0ull : ki[p];
+    }
   }
 }
 
@@ -1428,9 +1499,9 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
 
 // Part 3: refresh the block keys of the window rows (each (j0, j1) row is one contiguous i2 run),
 // then their superblock keys.  The whole workgroup calls it (at >= 0: the window's centre).
-__device__ void block_window_keys(const EArgs& a, const double* cache, const unsigned char* sel,
-                                  const ExactWS& w, long long nblk, long long at) {
-  const Window v = window_of(a, at);
+__device__ void block_window_keys_rows(const EArgs& a, const double* cache,
+                                       const unsigned char* sel, const ExactWS& w, long long nblk,
+                                       const Window& v) {
   const int wave = threadIdx.x >> 6, nwave = blockDim.x >> 6;
   const long long nrow = v.w0 * v.w1;
   for (long long rr = wave; rr < nrow; rr += nwave) {
@@ -1445,6 +1516,87 @@ __device__ void block_window_keys(const EArgs& a, const double* cache, const uns
     for (long long sb = y0 / EB / ESB; sb <= y1 / EB / ESB; ++sb)
       wave_super_key(w.bval, w.bidx, nblk, sb, w.sval, w.sidx);
   }
+  __syncthreads();
+}
+
+// Inclusive prefix sum over the wave (lane order).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  return x;
+}
+
+constexpr int WK_LIST = 128;  // distinct blocks / superblocks of a window handled by the list form
+
+// Part 3: refresh the block keys of the window rows (each (j0, j1) row is one contiguous i2 run),
+// then their superblock keys.  The whole workgroup calls it (at >= 0: the window's centre).  Rows
+// are increasing in y, so the blocks they touch form a sorted list with duplicates only between
+// neighbouring rows: wave 0 builds the DISTINCT blocks and superblocks (one row per lane, an
+// exclusive scan of the counts), then every block key is computed once — all of a wave's blocks'
+// entries loaded before any key is reduced — and every superblock key once.  (Row by row, a block
+// shared by two rows and a superblock shared by up to 36 were recomputed, each wave walking its
+// rows with one dependent load / reduce / store chain per block: 17 us per round at 128^3.)
+__device__ void block_window_keys(const EArgs& a, const double* cache, const unsigned char* sel,
+                                  const ExactWS& w, long long nblk, long long at) {
+  __shared__ long long s_blk[WK_LIST], s_sb[WK_LIST];
+  __shared__ int s_nb, s_ns;
+  const Window v = window_of(a, at);
+  const long long nrow = v.w0 * v.w1;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwave = blockDim.x >> 6;
+  if (nrow > 64 || v.w2 > EB) {
+    block_window_keys_rows(a, cache, sel, w, nblk, v);
+    return;
+  }
+  if (wave == 0) {
+    long long blo = 0, bhi = -1;
+    if (lane < nrow && v.w2 > 0) {
+      const long long y0 = ((v.lo0 + lane / v.w1) * a.I1 + v.lo1 + lane % v.w1) * a.I2 + v.lo2;
+      blo = y0 / EB;
+      bhi = (y0 + v.w2 - 1) / EB;
+    }
+    // the last block of the rows before (rows increase, so it is the previous lane's)
+    long long prev = __shfl_up(bhi, 1, 64);
+    if (lane == 0) prev = -1;
+    const long long own = max(blo, prev + 1);
+    const int nbl = bhi >= own ? (int)(bhi - own + 1) : 0;
+    const long long prev_sb = prev >= 0 ? prev / ESB : -1;
+    const long long sb0 = max(own / ESB, prev_sb + 1);
+    const int nsb_l = nbl > 0 && bhi / ESB >= sb0 ? (int)(bhi / ESB - sb0 + 1) : 0;
+    const int ib = wave_incl_scan(nbl), is = wave_incl_scan(nsb_l);
+    for (int q = 0; q < nbl; ++q)
+      if (ib - nbl + q < WK_LIST) s_blk[ib - nbl + q] = own + q;
+    for (int q = 0; q < nsb_l; ++q)
+      if (is - nsb_l + q < WK_LIST) s_sb[is - nsb_l + q] = sb0 + q;
+    if (lane == 63) {
+      s_nb = ib;
+      s_ns = is;
+    }
+  }
+  __syncthreads();
+  const int nb = s_nb, ns = s_ns;
+  if (nb > 4 * nwave || ns > WK_LIST) {  // (a window of more blocks than the fast form holds)
+    __syncthreads();
+    block_window_keys_rows(a, cache, sel, w, nblk, v);
+    return;
+  }
+  // blocks wave, wave + nwave, ...: at most 4 per wave
+  {
+    long long mine[4];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = wave + q * nwave;
+      mine[q] = j < nb ? s_blk[j] : 0;
+      cnt += j < nb;
+    }
+    if (cnt > 0) wave_block_keys<4>(cache, sel, a.n, mine, cnt, w.bval, w.bidx);
+  }
+  __syncthreads();
+  for (int j = wave; j < ns; j += nwave) wave_super_key(w.bval, w.bidx, nblk, s_sb[j], w.sval, w.sidx);
   __syncthreads();
 }
 
@@ -1752,7 +1904,7 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int nb, const int* slots,
     const long long side = std::min<long long>(2LL * (it + 1) * radius + 1, 2 * w.H + 1);
     const long long R = std::min<long long>(it + 1, w.H);
     const unsigned blocks = (unsigned)std::min<long long>(
-        CG_BLOCKS, oct ? ceil_div(2 * R * R + 2 * R + 1, (long long)(CG_T / 64))
+        CG_BLOCKS, oct ? ceil_div(2 * R * R + 2 * R + 1, (long long)(CG_T / 64 * CG_RPW))
                        : ceil_div(side * side * side, (long long)CG_T));
     if (oct) {
       hipLaunchKernelGGL(exact_cg_a_kernel<true>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
@@ -1903,8 +2055,8 @@ extern "C" int vgposp_exact_coef(VGPOSP_EXACT_PARAMS, void* stream) {
 }
 
 extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, const int* tab_nb,
-                                   const int* tab_cnt, int T, int K, double hi_scale, int64_t c0,
-                                   int64_t c1, void* stream) {
+                                   const int* tab_cnt, int T, int K, double hi_scale, double mu,
+                                   int64_t c0, int64_t c1, void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_bounds");
   VG_CHECK_ARG(tab_off != nullptr, 24);
   VG_CHECK_ARG(m == 1 || tab_nb != nullptr, 25);
@@ -1912,7 +2064,8 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   VG_CHECK_ARG(T >= 1 && T <= BND_TMAX && (int64_t)T * (m - 1) <= BND_NBMAX, 27);
   VG_CHECK_ARG(K >= 1 && K <= 4 * BND_SMAX, 28);
   VG_CHECK_ARG(hi_scale >= 1.0, 29);
-  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= a.n, 30);
+  VG_CHECK_ARG(mu >= 0.0, 30);
+  VG_CHECK_ARG(c0 >= 0 && c0 <= c1 && c1 <= a.n, 31);
   VG_CHECK_ARG(a.n < (1LL << 31), 3);
   if (c1 == c0) return 0;
   ProfScope ps("exact_bounds", s, 0.0, 0.0);
@@ -1924,7 +2077,8 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
 #define VG_BOUNDS_REG(SMV)                                                                       \
   if (T <= 64 * SMV) {                                                                           \
     hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6>), dim3(blocks), dim3(BND_T), 0, s, w.coef, \
-                       a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, lc0, lc1, out); \
+                       a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0, lc1,   \
+                       out);                                                                      \
     VG_LAUNCH_CHECK();                                                                           \
     return 0;                                                                                    \
   }
@@ -1938,7 +2092,7 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   }
 #undef VG_BOUNDS_REG
   hipLaunchKernelGGL(exact_bounds_kernel, dim3(blocks), dim3(BND_T), 0, s, w.coef, a.I0, a.I1, a.I2,
-                     a.m1, tab_off, tab_nb, tab_cnt, T, K, hi_scale, lc0, lc1, out);
+                     a.m1, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0, lc1, out);
   VG_LAUNCH_CHECK();
   return 0;
 }
@@ -2033,13 +2187,15 @@ extern "C" int vgposp_exact_buffers(void* ws, int64_t I0, int64_t I1, int64_t I2
 
 extern "C" int vgposp_exact_tighten_pending(VGPOSP_EXACT_PARAMS, const int* tab_off,
                                             const int* tab_nb, const int* tab_cnt, int T, int K,
-                                            double hi_scale, const int64_t* picks, void* stream) {
+                                            double hi_scale, double mu, const int64_t* picks,
+                                            void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_tighten_pending");
   VG_CHECK_ARG(tab_off != nullptr && tab_nb != nullptr && tab_cnt != nullptr, 24);
   VG_CHECK_ARG(T >= 1 && T <= BND_TMAX && (int64_t)T * (m - 1) <= BND_NBMAX, 27);
   VG_CHECK_ARG(K >= 1 && K <= 4 * BND_SMAX, 28);
   VG_CHECK_ARG(hi_scale >= 1.0, 29);
-  VG_CHECK_ARG(picks != nullptr, 30);
+  VG_CHECK_ARG(mu >= 0.0, 30);
+  VG_CHECK_ARG(picks != nullptr, 31);
   VG_CHECK_ARG(a.m1 == 6, 12);  // the register bounds kernel (the 7-point taper)
   const long long nblk = ceil_div(a.n, EB);
   double* out = const_cast<double*>(qdiag);
@@ -2049,8 +2205,8 @@ extern "C" int vgposp_exact_tighten_pending(VGPOSP_EXACT_PARAMS, const int* tab_
 #define VG_TIGHT_REG(SMV)                                                                        \
   if (T <= 64 * SMV) {                                                                           \
     hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6, true>), dim3(blocks), dim3(BND_T), 0, s,   \
-                       w.coef, a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, 0LL,   \
-                       0LL, out, w.rt_cand, w.ctl + CTL_NT);                                      \
+                       w.coef, a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu,    \
+                       0LL, 0LL, out, w.rt_cand, w.ctl + CTL_NT);                                 \
   } else
     VG_TIGHT_REG(4) VG_TIGHT_REG(6) VG_TIGHT_REG(9) VG_TIGHT_REG(14) {
       set_error("vgposp_exact_tighten_pending: reach table of %d nodes", T);

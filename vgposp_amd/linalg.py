@@ -235,9 +235,10 @@ def cholesky_(A, invert=False, check=True, ldiag=None):
     invert=False: lower(A) <- L;  invert=True: lower(A) <- L^-1.  The strictly upper triangle is
     untouched.  Returns (A, ldiag[B, n] = diag(L), info[B])."""
     A3, _ = _batched(A)
-    if not A3.is_contiguous():
-        raise ValueError("A must be contiguous")
     Bn, n = A3.shape[0], A3.shape[-1]
+    # rows contiguous; a padded row stride (lda > n) is allowed
+    if A3.stride(2) != 1 or A3.stride(1) < n or (Bn > 1 and A3.stride(0) < n * A3.stride(1)):
+        raise ValueError("A must have contiguous rows (row stride >= n, batch stride >= n * lda)")
     if ldiag is None:
         ldiag = torch.empty((Bn, n), dtype=F64, device=A3.device)
     info = torch.empty(Bn, dtype=torch.int32, device=A3.device)

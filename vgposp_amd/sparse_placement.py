@@ -445,6 +445,15 @@ def bound_steps(offsets, lam_min, lam_max, target=1e-6, kmax=12):
     return best
 
 
+def radau_steps(b):
+    """The Gauss-Radau form of a Chebyshev (K, hi_scale, width) triple: K - 1 steps (at least 1),
+    hi_scale = the rounding margin only, width = the Chebyshev width of K steps (the Radau
+    bracket after K - 1 steps measures about that on the beta = 4 taper; informational only —
+    the bound is valid whatever its width)."""
+    K, _, width = b
+    return (max(1, K - 1), 1.0 + BOUND_MARGIN, width)
+
+
 class ExactWindowGreedy:
     """The rounds of algorithm 3 on a TaperProblem: given diag(Q) (``run``, after the selected
     inverse), or with diag(Q) only bounded (``run_bounded``, after ``bound_qdiag``)."""
@@ -471,7 +480,14 @@ class ExactWindowGreedy:
         self.refine_batches = 0   # batched CG solves in the last bounded run
         self.bound = None
         self.tight = None
-        self.two_level = True     # bound_qdiag's default: two bound levels (7-point stencils)
+        # bound_qdiag's default: ONE bound level.  With the Gauss-Radau bounds one level of K = 4
+        # steps (bracket ~9e-7) runs the 128^3 k = 50 case in 7.3 ms against 8.7 ms for two
+        # levels (K = 3 for all, K = 5 before a CG column): the second level's extra refinement
+        # events (6 host round trips and top-B selections instead of 3) cost more than its
+        # cheaper first pass saves (profiles/r4_c4_radau.jsonl)
+        self.two_level = False
+        self.radau = True         # Gauss-Radau upper bounds (mu = the Gershgorin lambda_min)
+        self.bound_mu = 0.0       # mu of the last bounds (0: the Chebyshev bound)
         self.tightened = 0        # candidates tightened to the K_hi bound in the last bounded run
 
     def _args(self, qdiag):
@@ -506,10 +522,13 @@ class ExactWindowGreedy:
         g = self.ws[off: off + 16].view(torch.float64).cpu()
         return float(g[0]), float(g[1])
 
-    def bound_qdiag(self, qdiag, c0=0, c1=None, steps=None, tighten=None):
+    def bound_qdiag(self, qdiag, c0=0, c1=None, steps=None, tighten=None, mu=0.0):
         """qdiag[c0:c1] <- upper bounds of Q_yy (vgposp_exact_bounds).  Returns the (K, hi_scale,
         width) used, or None when the spectrum bounds cannot bracket Q_yy (then the selected
-        inverse is the only exact route).  With ``tighten`` (7-point stencils) the bounds are
+        inverse is the only exact route).  ``steps``: an explicit (K, hi_scale, width) triple,
+        with ``mu`` > 0 its Gauss-Radau form (default: the Chebyshev form); otherwise the steps
+        are chosen here, in the Gauss-Radau form when ``self.radau``.  With ``tighten`` (7-point
+        stencils) the bounds are
         the K_lo-step ones and run_bounded tightens candidates to K_hi steps before their CG
         column (``self.tight`` = the K_hi triple, None when there is no second level; default
         ``self.two_level``)."""
@@ -521,14 +540,23 @@ class ExactWindowGreedy:
             b = steps
         else:
             b = bound_steps(offs, lo, hi, target=BOUND_LO_TARGET if two else 1e-6)
-        self.bound = b
         self.tight = None
+        self.bound_mu = float(mu) if steps is not None else 0.0
         if b is None:
+            self.bound = None
             return None
         if two:
             t = bound_steps(offs, lo, hi, target=BOUND_HI_TARGET)
             if t is not None and t[0] > b[0]:
                 self.tight = t
+        if self.radau and steps is None:
+            # the Gauss-Radau bound brackets after K steps about as tightly as the Chebyshev one
+            # after K + 1 (exact_greedy.hip, radau_step): one CG step fewer for the same width
+            self.bound_mu = lo
+            b = radau_steps(b)
+            if self.tight is not None:
+                self.tight = radau_steps(self.tight)
+        self.bound = b
         # the measured spectrum bounds are tighter than the kernel-agnostic one the columns were
         # sized with: fewer CG iterations (and a smaller Krylov box) give the same tolerance
         its = cg_iterations_for(lo, hi, self.cg_tol)
@@ -539,7 +567,7 @@ class ExactWindowGreedy:
         tab, T = self._device_table(K)
         c1 = self.p.n if c1 is None else int(c1)
         call("vgposp_exact_bounds", *self._args(qdiag), *[_p(a) for a in tab], T, K, scale,
-             int(c0), c1, _stream())
+             self.bound_mu, int(c0), c1, _stream())
         return b
 
     def _device_table(self, K):
@@ -584,7 +612,7 @@ class ExactWindowGreedy:
         pk, pd = _p(self.picks), _p(self.pick_delta)
         if tight is not None:
             ttab, tT = self._device_table(tight[0])
-            targs = (*[_p(a) for a in ttab], tT, tight[0], tight[1], pk)
+            targs = (*[_p(a) for a in ttab], tT, tight[0], tight[1], self.bound_mu, pk)
         call("vgposp_exact_steps", *args, 0, 1, k, B, pk, pd, st)  # round 0 stalls: nothing refined
         issued, reads = 1, 0
         while True:
