@@ -511,8 +511,11 @@ def c4_roofline(run, prof, ncand, pmc_path=None):
         steps (T rows of m doubles: its K-step Krylov space) and writes qdiag[y].  Unique bytes
         (the coefficient table once + qdiag) against HBM; the per-candidate operand bytes
         (T m 8 + 8) against the L2, where the neighbouring candidates' shared rows are served.
-      exact_cg: per column and iteration the active cube of (it + 1) stencil radii around the
-        column's centre, 8 (m + 9) bytes per node (coefficient row, r / p / q / x reads and writes).
+      exact_cg: per column and iteration the active region of (it + 1) stencil radii around the
+        column's centre — the Manhattan ball (2R + 1)(2R^2 + 2R + 3) / 3 nodes for the 7-point
+        stencil, whose CG walk skips the rest of the cube; the cube otherwise — at 8 (m + 9) bytes
+        per node (coefficient row, r / p / q / x reads and writes), every column counted for the
+        iteration cap (columns that converge earlier exit early, so this over-counts).
     `traffic`: FETCH + WRITE bytes per run from a rocprofv3 PMC pass (profiles/pmc_c4_*.json) when
     it was measured on this build's sources."""
     from vgposp_amd._lib import source_hash
@@ -536,7 +539,11 @@ def c4_roofline(run, prof, ncand, pmc_path=None):
         out["l2_frac"] = out["l2_achieved"] / L2_PEAK_GBS
     cg_ms = prof.get("exact_cg", (0.0,))[0]
     box = 2 * g.radius * g.cg_iters + 1
-    node_its = sum(min(2 * (it + 1) * g.radius + 1, box) ** 3 for it in range(g.cg_iters))
+    if m == 7 and g.radius == 1:  # the 7-point walk covers the diamond |d0| + |d1| + |d2| <= R
+        node_its = sum((2 * R + 1) * (2 * R * R + 2 * R + 3) // 3
+                       for R in (min(it + 1, g.cg_iters) for it in range(g.cg_iters)))
+    else:
+        node_its = sum(min(2 * (it + 1) * g.radius + 1, box) ** 3 for it in range(g.cg_iters))
     cg_bytes = g.refinements * node_its * 8.0 * (m + 9)
     out["cg"] = {"kernel": "exact_cg_a/b", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                  "columns": g.refinements, "iterations": g.cg_iters, "batches": g.refine_batches,

@@ -22,12 +22,19 @@ if args[:1] == ["--reps"]:
     REPS, args = int(args[1]), args[2:]
 ONE = "--two-level" not in args  # (the default is one bound level)
 CHEB = "--cheb" in args  # the Chebyshev bounds (K + 1 steps) instead of Gauss-Radau
+TARGET = None
+if "--target" in args:  # the one-level bracket target (Chebyshev width), e.g. 3e-5 -> K = 3 Radau
+    i = args.index("--target")
+    TARGET = float(args[i + 1])
+    args = args[:i] + args[i + 2:]
 args = [a for a in args if a not in ("--one-level", "--two-level", "--cheb")]
 X, shape, ls = c4_grid()
 run = ExactTaperPlacement(X, shape, 50, 3, 4.0, ls=ls, diag_shift=0.01 + 1e-6, method="bounds")
 g = run.greedy
 g.two_level = not ONE
 g.radau = not CHEB
+if TARGET is not None:
+    g.bound_target = TARGET
 for B in [int(v) for v in args] or [8]:
     orig = g.run_bounded
     g.run_bounded = lambda q, k, _o=orig, _b=B: _o(q, k, batch=_b)

@@ -472,6 +472,19 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
       nbo[s][o] = lo | (hi << 16);
     }
   const char* plb = reinterpret_cast<const char*>(pl);
+  // the lane's table offsets, likewise once: three signed bytes per slot (|offset| <= K <= 56)
+  int ofr[SM];
+#pragma unroll
+  for (int s = 0; s < SM; ++s) {
+    const int j = s * 64 + lane;
+    ofr[s] = j < T ? ((offl[3 * j] + 128) | ((offl[3 * j + 1] + 128) << 8) |
+                      ((offl[3 * j + 2] + 128) << 16))
+                   : -1;
+  }
+  // 32-bit grid arithmetic (n < 2^31, checked by the caller): the 64-bit divisions and products
+  // of the candidate's coordinates and its rows' indices were a large part of a candidate's cost
+  const int I0i = (int)I0, I1i = (int)I1, I2i = (int)I2;
+  const unsigned I12 = (unsigned)(I1i * I2i);
   // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so XCD x (= blockIdx.x
   // mod 8) walks its own contiguous eighth of the candidates and neighbouring candidates, whose
   // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
@@ -491,24 +504,28 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
        it_y += LIST ? (long long)gridDim.x * BND_WAVES : (long long)(gridDim.x >> 3) * BND_WAVES) {
     const long long y = LIST ? list[it_y] : it_y;
 #endif
-    const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
+    const unsigned yu = (unsigned)y;
+    const int y0 = (int)(yu / I12), yr = (int)(yu - (unsigned)y0 * I12);
+    const int y1 = yr / I2i, y2 = yr - y1 * I2i;
     double c[SM][M];
     double r[SM], p[SM], q[SM];
 #pragma unroll
     for (int s = 0; s < SM; ++s) {
       const int j = s * 64 + lane;
-      long long gi = -1;
-      if (j < T) {
-        const long long g0 = y0 + offl[3 * j], g1 = y1 + offl[3 * j + 1], g2 = y2 + offl[3 * j + 2];
-        if (g0 >= 0 && g0 < I0 && g1 >= 0 && g1 < I1 && g2 >= 0 && g2 < I2)
-          gi = (g0 * I1 + g1) * I2 + g2;
+      int gi = -1;
+      if (ofr[s] >= 0) {
+        const int g0 = y0 + (ofr[s] & 255) - 128, g1 = y1 + ((ofr[s] >> 8) & 255) - 128,
+                  g2 = y2 + ((ofr[s] >> 16) & 255) - 128;
+        if ((unsigned)g0 < (unsigned)I0i && (unsigned)g1 < (unsigned)I1i &&
+            (unsigned)g2 < (unsigned)I2i)
+          gi = (g0 * I1i + g1) * I2i + g2;
       }
       // the padded row in two-double loads
       constexpr int MS = coef_stride(M);
 #pragma unroll
       for (int o = 0; o < MS; o += 2) {
         double2 v = make_double2(0.0, 0.0);
-        if (gi >= 0) v = *reinterpret_cast<const double2*>(coef + gi * MS + o);
+        if (gi >= 0) v = *reinterpret_cast<const double2*>(coef + (size_t)gi * MS + o);
         if (o < M) c[s][o] = v.x;
         if (o + 1 < M) c[s][o + 1] = v.y;
       }
@@ -998,7 +1015,7 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
 // for B = 32.)
 template <int P>
 __device__ __forceinline__ void wave_topb(double (&v)[P], long long (&id)[P], int B, double* ov,
-                                          long long* oi) {
+                                          long long* oi, int* taken = nullptr) {
   const int lane = threadIdx.x & 63;
   // the branch-free encoded order, held as two plain arrays and selected component-wise (an
   // array of Key structs selected as a whole went through scratch memory: 540 us per stall)
@@ -1026,10 +1043,18 @@ __device__ __forceinline__ void wave_topb(double (&v)[P], long long (&id)[P], in
       ki[p] = hit ? 0ull : ki[p];
     }
   }
+  if (taken) {  // bit p: item p was among the B taken
+    int m = 0;
+#pragma unroll
+    for (int p = 0; p < P; ++p) m |= (id[p] >= 0 && ki[p] == 0ull) ? (1 << p) : 0;
+    *taken = m;
+  }
 }
 
 // The B best of `count` items (key(i, v, idx), i < count <= P * SEL_THREADS) -> out[0] = how many
 // (<= B), out[1 ..] = their indices, best first.  sv / si: LDS scratch [16 B].  Whole workgroup.
+constexpr int TOPW = 8;  // block_topb_keys' first pass: each wave's best TOPW
+
 template <int P, class KeyFn>
 __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long long* si,
                                long long* out) {
@@ -1043,6 +1068,49 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
     v[p] = 0.0;
     id[p] = -1;
     if (i < count) key(i, v[p], id[p]);
+  }
+  // Pass 1: each wave's best TOPW entries, merged by wave 0.  The merged top B is exact unless
+  // some wave had all TOPW of its entries taken (it may hold more of the top B): only then every
+  // wave extracts its best B (pass 2).  (B passes of a wave arg-max per wave were 170 us of a
+  // stall at 128^3; the first pass alone is a quarter of that.)
+  __shared__ int s_full;
+  if (B > TOPW) {
+    wave_topb<P>(v, id, TOPW, sv + wave * TOPW, si + wave * TOPW);
+    __syncthreads();
+    if (wave == 0) {
+      constexpr int Q1 = NW * TOPW / 64;  // items per lane; lanes 4s .. 4s + 3 hold wave s's
+      static_assert(Q1 == 2 && TOPW == 8, "merge layout: two items per lane, four lanes per wave");
+      double v1[Q1];
+      long long id1[Q1];
+      const int lane = t & 63;
+#pragma unroll
+      for (int q = 0; q < Q1; ++q) {
+        v1[q] = sv[lane * Q1 + q];
+        id1[q] = si[lane * Q1 + q];
+      }
+      int tk = 0;
+      wave_topb<Q1>(v1, id1, B, sv + NW * CG_B, si + NW * CG_B, &tk);
+      const unsigned long long m0 = __ballot(tk & 1), m1 = __ballot(tk & 2);
+      int full = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        full |= (((m0 >> (4 * w)) & 0xFull) == 0xFull) && (((m1 >> (4 * w)) & 0xFull) == 0xFull);
+      if (lane == 0) s_full = full;
+    }
+    __syncthreads();
+    if (!s_full) {
+      if (wave == 0 && (t & 63) == 0) {
+        int c = 0;
+        for (int b = 0; b < B; ++b) {
+          const long long k = si[NW * CG_B + b];
+          if (k < 0) break;
+          out[1 + c++] = k;
+        }
+        out[0] = c;
+      }
+      __syncthreads();
+      return (int)out[0];
+    }
   }
   wave_topb<P>(v, id, B, sv + wave * B, si + wave * B);
   __syncthreads();
@@ -1127,6 +1195,7 @@ __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int n
 
 constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in config C4)
 constexpr int EX_SLOTS_MAX = 2 * EX_KMAX;  // column slots (exact_slots(kmax) <= this)
+constexpr int ROWS_LDS = 8192;  // doubles: packed rows of both factors (each half) up to |A| = 90
 
 // (A/B builds only, -DVGPOSP_EXACT_DBG=1: thread 0 of the per-round kernels stamps its phases with
 // the 100 MHz real-time counter; vgposp_exact_dbg copies the last 64 records out.)
@@ -1168,6 +1237,8 @@ __device__ __forceinline__ FactorRows global_rows(const ExactWS& w, int km) {
 
 // Stage rows 0 .. nr-1 of both factors as packed lower triangles into sm (2 nr (nr + 1) / 2
 // doubles), the whole workgroup.
+// (LQ's packed rows at sm, LS's at sm + ROWS_LDS / 2, so a row appended later lands in place;
+// nr (nr + 1) <= ROWS_LDS)
 __device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int km, int nr, double* sm) {
   const int np = nr * (nr + 1) / 2;
   for (int e = threadIdx.x; e < 2 * np; e += blockDim.x) {
@@ -1176,10 +1247,10 @@ __device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int km, int n
     while (r * (r + 1) / 2 > k) --r;
     while ((r + 1) * (r + 2) / 2 <= k) ++r;
     const int s = k - r * (r + 1) / 2;
-    sm[e] = (which ? w.LS : w.LQ)[(size_t)r * km + s];
+    sm[which ? ROWS_LDS / 2 + k : k] = (which ? w.LS : w.LQ)[(size_t)r * km + s];
   }
   __syncthreads();
-  return FactorRows{sm, sm + np, 0};
+  return FactorRows{sm, sm + ROWS_LDS / 2, 0};
 }
 
 // What a re-score needs of pick r, staged in LDS once per workgroup: its grid coordinates and
@@ -1394,22 +1465,17 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_tighten_end_kernel(EArgs a,
 // After q_t = Q e_{a_t}, part 1: row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I) (one wave
 // each; the earlier rows staged in LDS when they fit, the right-hand sides computed by all lanes
 // at once, then one forward substitution with lane s holding z_s).
-constexpr int ROWS_LDS = 8192;  // doubles: packed rows of both factors up to |A| = 63
 
 // Row `round` of both factors, the whole workgroup (>= 128 threads) calling: waves 0 and 1 compute
 // (LQ / LS), every thread stages the earlier rows.
+// Row `round` of LQ (wave 0) / LS (wave 1) from the staged picks and rows 0 .. round - 1 in L:
+// written to the workspace, and with lds_rows (the staged packed rows, L.stride == 0) appended
+// there too.
 template <int KIND>
-__device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
-                                  const long long* picks, double* sm) {
+__device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const FactorRows& L,
+                             const StagedPicks& sp, double* lds_rows) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int km = a.kmax;
-  const long long at = picks[round];
-  if (at < 0) return;
-  __shared__ StagedPicks sp;
-  stage_picks(a, w, picks, round + 1, sp);
-  const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, km, round, sm)
-                                                        : (__syncthreads(), global_rows(w, km));
-  if (wave > 1) return;
   const double* Lm = wave == 0 ? L.lq : L.ls;
   // (the staged forms of qcol_at(w, round, picks[r]) and sigma_off(a, at, picks[r]))
   auto val = [&](int r) {
@@ -1438,8 +1504,31 @@ __device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
   if (lane + 64 < round) Lw[lane + 64] = z1;
   // diagonal: sqrt(v_round - |z|^2), v_round held by lane round % 64
   const double vr = wave_bcast(round < 64 ? v0 : v1, round & 63);
-  if (lane == 0) Lw[round] = sqrt(vr - nz);
+  const double dg = sqrt(vr - nz);
+  if (lane == 0) Lw[round] = dg;
+  if (lds_rows) {
+    double* Ll = lds_rows + (wave == 0 ? 0 : ROWS_LDS / 2) + round * (round + 1) / 2;
+    if (lane < round) Ll[lane] = z0;
+    if (lane + 64 < round) Ll[lane + 64] = z1;
+    if (lane == 0) Ll[round] = dg;
+  }
 }
+
+template <int KIND>
+__device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
+                                  const long long* picks, double* sm) {
+  const int wave = threadIdx.x >> 6;
+  const int km = a.kmax;
+  const long long at = picks[round];
+  if (at < 0) return;
+  __shared__ StagedPicks sp;
+  stage_picks(a, w, picks, round + 1, sp);
+  const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, km, round, sm)
+                                                        : (__syncthreads(), global_rows(w, km));
+  if (wave > 1) return;
+  wave_new_row<KIND>(a, w, round, L, sp, nullptr);
+}
+
 
 template <int KIND>
 __global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int round,
@@ -1476,11 +1565,17 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
   const long long at = picks[round];
   if (at < 0) return;
   const Window v = window_of(a, at);
-  // every candidate of the workgroup walks the same factor rows and picks: stage them once
+  // every candidate of the workgroup walks the same factor rows and picks: stage them once.  The
+  // pick's own rows (row `round` of LQ and LS) are computed HERE, by waves 0 and 1 of every
+  // workgroup (the same values, so the same bits written to the workspace), instead of by the
+  // single-workgroup step kernel before this launch: 9 us per round off the critical path
   const int nr = round + 1;
   stage_picks(a, w, picks, nr, sp);
-  const FactorRows L = nr * (nr + 1) <= ROWS_LDS ? stage_rows(w, a.kmax, nr, sm)
-                                                 : (__syncthreads(), global_rows(w, a.kmax));
+  const bool lds = nr * (nr + 1) <= ROWS_LDS;
+  const FactorRows L = lds ? stage_rows(w, a.kmax, round, sm)
+                           : (__syncthreads(), global_rows(w, a.kmax));
+  if ((threadIdx.x >> 6) < 2) wave_new_row<KIND>(a, w, round, L, sp, lds ? sm : nullptr);
+  __syncthreads();
   const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (e >= v.w0 * v.w1 * v.w2) return;
   const long long y = ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) * a.I2 +
@@ -1932,10 +2027,12 @@ int exact_update_t(const EArgs& a, const double* qdiag, double* cache, unsigned 
                    const ExactWS& w, int round, const long long* picks, hipStream_t s) {
   const long long nblk = ceil_div(a.n, EB);
   ProfScope ps("exact_update", s, 0.0, 0.0);
-  hipLaunchKernelGGL(exact_rows_kernel<KIND>, dim3(1), dim3(128), 0, s, a, w, round, picks);
-  VG_LAUNCH_CHECK();
   const long long side = 2LL * a.cutoff;
   const long long nw = side * side * side;
+  if (nw <= 0) {  // (otherwise the window kernel computes the pick's factor rows)
+    hipLaunchKernelGGL(exact_rows_kernel<KIND>, dim3(1), dim3(128), 0, s, a, w, round, picks);
+    VG_LAUNCH_CHECK();
+  }
   if (nw > 0) {
     hipLaunchKernelGGL(exact_window_kernel<KIND>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, s,
                        a, qdiag, cache, sel, w, round, picks);
@@ -2122,9 +2219,10 @@ extern "C" int vgposp_exact_steps(VGPOSP_EXACT_PARAMS, int round0, int round1, i
       const bool more = r + 1 < k;  // the last pick needs neither factor rows nor a window
       {
         ProfScope ps("exact_select", s, 0.0, 16.0 * nsb);
+        // (the factor rows of pick r: in the window kernel, here only when there is no window)
         hipLaunchKernelGGL(exact_step_kernel<KD>, dim3(1), dim3(SEL_THREADS), 0, s, a, cache,
-                           selected, w, nblk, nsb, exact_slots(kmax), r, batch, (int)more, pk,
-                           pick_delta);
+                           selected, w, nblk, nsb, exact_slots(kmax), r, batch,
+                           (int)(more && nw <= 0), pk, pick_delta);
         VG_LAUNCH_CHECK();
       }
       if (more && nw > 0) {  // the window of pick r (no-op when the round stalled: picks[r] = -1)
@@ -2197,6 +2295,7 @@ extern "C" int vgposp_exact_tighten_pending(VGPOSP_EXACT_PARAMS, const int* tab_
   VG_CHECK_ARG(mu >= 0.0, 30);
   VG_CHECK_ARG(picks != nullptr, 31);
   VG_CHECK_ARG(a.m1 == 6, 12);  // the register bounds kernel (the 7-point taper)
+  VG_CHECK_ARG(a.n < (1LL << 31), 3);
   const long long nblk = ceil_div(a.n, EB);
   double* out = const_cast<double*>(qdiag);
   const unsigned blocks = (unsigned)ceil_div(CG_B, BND_WAVES);

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
 static size_t leaf_shmem() { return (size_t)NB * LP2 * sizeof(double); }
 
 // A (jb x jb lower) <- linv (the saved leaf inverse); batch element blockIdx.y at the strides
-__global__ void copy_leaf_kernel(double* A, int64_t lda, int jb, const double* linv,
+__global__ __launch_bounds__(256) void copy_leaf_kernel(double* A, int64_t lda, int jb, const double* linv,
                                  int64_t sA = 0, int64_t sL = 0) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   A += blockIdx.y * sA;
@@ -384,7 +384,7 @@ static int pgemm(const Fact& f, int transa, int transb, int64_t m, int64_t n, in
 
 // dst (n x n lower, ldd) <- src (lower, lds); zero_upper: also zero dst's strict upper triangle
 // (dst is then a full-matrix GEMM operand); otherwise dst's upper triangle is left untouched.
-__global__ void copy_lower_kernel(double* dst, int64_t ldd, const double* src, int64_t lds,
+__global__ __launch_bounds__(256) void copy_lower_kernel(double* dst, int64_t ldd, const double* src, int64_t lds,
                                   int64_t n, int zero_upper, int64_t sd = 0, int64_t ss = 0) {
   const int64_t r = blockIdx.y;
   dst += blockIdx.z * sd;

@@ -487,6 +487,7 @@ class ExactWindowGreedy:
         # cheaper first pass saves (profiles/r4_c4_radau.jsonl)
         self.two_level = False
         self.radau = True         # Gauss-Radau upper bounds (mu = the Gershgorin lambda_min)
+        self.bound_target = 1e-6  # one-level bracket target (Chebyshev width; Radau: one step less)
         self.bound_mu = 0.0       # mu of the last bounds (0: the Chebyshev bound)
         self.tightened = 0        # candidates tightened to the K_hi bound in the last bounded run
 
@@ -539,7 +540,7 @@ class ExactWindowGreedy:
         if steps is not None:
             b = steps
         else:
-            b = bound_steps(offs, lo, hi, target=BOUND_LO_TARGET if two else 1e-6)
+            b = bound_steps(offs, lo, hi, target=BOUND_LO_TARGET if two else self.bound_target)
         self.tight = None
         self.bound_mu = float(mu) if steps is not None else 0.0
         if b is None:
