@@ -531,6 +531,12 @@ int vgposp_front_diag(const double* QPP, int64_t p, int nf, const int* piv, doub
  *   vgposp_exact_tighten_pending: the tightening list's bounds again with the K_hi-step table
  *     (arguments as vgposp_exact_bounds; the smaller of the two bounds is kept), the candidates'
  *     cache entries re-scored; clears the stall when the CG batch is empty.  m = 7 only.
+ *   vgposp_exact_pretighten: after prepare(flags = 3) and steps_reset, before the rounds: the
+ *     M <= 32,768 candidates with the largest round-0 entries (a radix select of the M-th largest
+ *     key; ties at the threshold included; if that lists more than 65,536, none) get the K_hi-step
+ *     bounds at once
+ *     (arguments as vgposp_exact_bounds), their entries re-scored and the arg-max keys rebuilt;
+ *     the count is added to the control block's tightened total.  m = 7 only.
  *   vgposp_exact_refine_pending: Q e_c for the pending CG batch by one batched CG (columns into
  *     their slots); each Q_cc becomes exact and the candidate's cache entry the reference's value
  *     (scored with the A of its last re-score); clears the stall.  After the tightening when both
@@ -572,6 +578,9 @@ int vgposp_exact_refine_pending(VGPOSP_EXACT_ARGS, int batch, const int64_t* pic
 int vgposp_exact_tighten_pending(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
                                  const int* tab_cnt, int T, int K, double hi_scale, double mu,
                                  const int64_t* picks, void* stream);
+int vgposp_exact_pretighten(VGPOSP_EXACT_ARGS, const int* tab_off, const int* tab_nb,
+                            const int* tab_cnt, int T, int K, double hi_scale, double mu,
+                            int64_t M, void* stream);
 int vgposp_exact_ctl(void* ws, int64_t I0, int64_t I1, int64_t I2, int m, int kmax, int radius,
                      int cg_iters, int** ctl);
 int vgposp_exact_update(VGPOSP_EXACT_ARGS, int round, const int64_t* picks, void* stream);

@@ -111,21 +111,26 @@ def test_bounded_alg3_matches_oracle(shape, k, cutoff, beta, kind):
     assert g.refine_batches <= 2 * k and k <= g.refinements <= REFINE_BATCH * g.refine_batches
 
 
-@pytest.mark.parametrize("shape,k,cutoff,kind", [
-    ((14, 13, 12), 30, 3, "matern32"),
-    ((20, 16, 14), 40, 2, "eq"),
+@pytest.mark.parametrize("shape,k,cutoff,kind,pre", [
+    ((14, 13, 12), 30, 3, "matern32", 0),
+    ((20, 16, 14), 40, 2, "eq", 0),
+    ((20, 16, 14), 40, 2, "eq", 24),
+    ((14, 13, 12), 30, 3, "matern32", 300),
+    ((20, 16, 14), 40, 3, "eq", 100000),
 ])
-def test_two_bound_levels_equal_one(shape, k, cutoff, kind):
-    """The K_lo bounds + tightening to K_hi before a CG column, and one K = 5 level for all: the
-    same picks and pick deltas (bit for bit: every pick's delta comes from its exact Q_yy either
-    way), the oracle's picks."""
-    from vgposp_amd.sparse_placement import ExactTaperPlacement
+def test_two_bound_levels_equal_one(shape, k, cutoff, kind, pre):
+    """The K_lo bounds + tightening to K_hi before a CG column (on demand, and with the `pre`
+    best round-0 candidates tightened before the rounds: a few, some hundreds, all), and one
+    bound level for all: the same picks and pick deltas (bit for bit: every pick's delta comes
+    from its exact Q_yy either way), the oracle's picks."""
+    from vgposp_amd.sparse_placement import PRETIGHTEN, ExactTaperPlacement
     X, ls = _grid(shape, seed=k + 3)
     out = []
     for two in (True, False):
         run = ExactTaperPlacement(X, shape, k, cutoff, 4.0, kind, ls=ls, diag_shift=SHIFT,
                                   method="bounds")
         run.greedy.two_level = two
+        run.greedy.pretighten = min(pre, 32768)
         A = [int(a) for a in run.run().cpu().numpy()]
         g = run.greedy
         assert (g.tight is not None) == two
@@ -133,6 +138,9 @@ def test_two_bound_levels_equal_one(shape, k, cutoff, kind):
     assert out[0][0] == out[1][0]
     np.testing.assert_array_equal(out[0][1], out[1][1])
     assert out[0][2] > 0 and out[1][2] == 0
+    if pre:  # at least the pre-tightened ones (every candidate when pre >= n)
+        assert out[0][2] >= min(pre, int(np.prod(shape)))
+    assert 1 <= PRETIGHTEN <= 65536
     rA, _, _ = op.placement_window_precision(_dense(X, shape, 4.0, ls, kind), k, shape, cutoff)
     assert out[0][0] == rA
 

@@ -1,5 +1,5 @@
 """C4 (128^3, k = 50, beta 4, cutoff 3) end-to-end run time, as bench.py's c4 line measures it:
-python tools/c4_time.py [--reps R] [--two-level] [--cheb] [batch ...] -> one JSON line per refinement batch size: mean ms
+python tools/c4_time.py [--reps R] [--one-level] [--cheb] [batch ...] -> one JSON line per refinement batch size: mean ms
 over R (10) runs, picks vs tests/golden/c4_picks.json, refinements / batches / host reads, and a profiled run's
 per-phase event times.  --one-level: one bound level for all candidates (no tightening)."""
 import json
@@ -20,12 +20,21 @@ args = sys.argv[1:]
 REPS = 10
 if args[:1] == ["--reps"]:
     REPS, args = int(args[1]), args[2:]
-ONE = "--two-level" not in args  # (the default is one bound level)
+ONE = "--one-level" in args  # (the default is two bound levels)
 CHEB = "--cheb" in args  # the Chebyshev bounds (K + 1 steps) instead of Gauss-Radau
 TARGET = None
 if "--target" in args:  # the one-level bracket target (Chebyshev width), e.g. 3e-5 -> K = 3 Radau
     i = args.index("--target")
     TARGET = float(args[i + 1])
+    args = args[:i] + args[i + 2:]
+PT = LOT = None
+if "--pt" in args:  # two levels: candidates pre-tightened before the rounds
+    i = args.index("--pt")
+    PT = int(args[i + 1])
+    args = args[:i] + args[i + 2:]
+if "--lo-target" in args:  # two levels: the first level's bracket target (Chebyshev width)
+    i = args.index("--lo-target")
+    LOT = float(args[i + 1])
     args = args[:i] + args[i + 2:]
 args = [a for a in args if a not in ("--one-level", "--two-level", "--cheb")]
 X, shape, ls = c4_grid()
@@ -35,6 +44,10 @@ g.two_level = not ONE
 g.radau = not CHEB
 if TARGET is not None:
     g.bound_target = TARGET
+if PT is not None:
+    g.pretighten = PT
+if LOT is not None:
+    g.lo_target = LOT
 for B in [int(v) for v in args] or [8]:
     orig = g.run_bounded
     g.run_bounded = lambda q, k, _o=orig, _b=B: _o(q, k, batch=_b)
@@ -54,7 +67,7 @@ for B in [int(v) for v in args] or [8]:
     prof = _lib.prof_dump()
     _lib.prof_enable(False)
     g.run_bounded = orig
-    print(json.dumps({"batch": B, "levels": 1 if ONE else 2, "radau": g.radau, "bound": g.bound, "tight": g.tight,
+    print(json.dumps({"batch": B, "levels": 1 if ONE else 2, "radau": g.radau, "pretighten": g.pretighten, "bound": g.bound, "tight": g.tight,
                       "tightened": g.tightened, "ms_mean": 1e3 * sum(ts) / len(ts), "ms_min": 1e3 * min(ts),
                       "picks_equal": picks == want, "refinements": g.refinements,
                       "batches": g.refine_batches, "host_reads": getattr(g, "host_reads", None),

@@ -147,6 +147,8 @@ SIGNATURES = {
     "vgposp_exact_refine_pending": (_i32, _EXACT + [_i32, _c_void_p, _f64, _c_void_p]),
     "vgposp_exact_tighten_pending": (_i32, _EXACT + [_c_void_p, _c_void_p, _c_void_p, _i32, _i32,
                                                      _f64, _f64, _c_void_p, _c_void_p]),
+    "vgposp_exact_pretighten": (_i32, _EXACT + [_c_void_p, _c_void_p, _c_void_p, _i32, _i32,
+                                                _f64, _f64, _i64, _c_void_p]),
     "vgposp_exact_ctl": (_i32, [_c_void_p, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                                 ctypes.POINTER(_c_void_p)]),
     "vgposp_exact_update": (_i32, _EXACT + [_i32, _c_void_p, _c_void_p]),

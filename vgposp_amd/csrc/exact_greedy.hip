@@ -88,6 +88,11 @@ struct ExactWS {
   long long* rf_cand; // [CG_B]: the pending refinement batch (-1: unused column)
   int* rf_slot;       // [CG_B]
   long long* rt_cand; // [CG_B]: the pending tightening list (ctl[CTL_NT] entries)
+  // pre-tightening (vgposp_exact_pretighten): the best candidates of round 0 tightened at once
+  long long* pt_list;      // [PT_MAX]
+  unsigned* pt_hist;       // [PT_BINS] radix-select histogram
+  long long* pt_state;     // [4]: threshold code, candidates still needed, pass, listed count
+  int* pt_count;           // [1]: list entries (<= PT_MAX), as the LIST bounds kernel reads it
   size_t bytes;
 };
 
@@ -107,6 +112,9 @@ __host__ __device__ constexpr int coef_stride(int m) { return (m + 1) & ~1; }
 
 // column slots: one per pick, as many again for refined candidates that are not (yet) picked
 __host__ __device__ __forceinline__ int exact_slots(int kmax) { return 2 * kmax; }
+
+constexpr int PT_BINS = 4096;          // 12-bit digits of the radix select
+constexpr long long PT_MAX = 65536;    // candidates pre-tightened per run (at most)
 
 constexpr int CG_MAXIT = 512;
 constexpr int CG_B = 32;      // columns solved together by one batched CG (blockIdx.y)
@@ -158,6 +166,10 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
   w.rl_pin = (unsigned char*)take((size_t)exact_slots(kmax));
   w.rf_cand = (long long*)take(8 * CG_B);
   w.rf_slot = (int*)take(4 * CG_B);
+  w.pt_list = (long long*)take(8 * (size_t)PT_MAX);
+  w.pt_hist = (unsigned*)take(4 * (size_t)PT_BINS);
+  w.pt_state = (long long*)take(8 * 4);
+  w.pt_count = (int*)take(16);
   w.rt_cand = (long long*)take(8 * CG_B);
   w.bytes = off;
   return w;
@@ -598,6 +610,112 @@ __global__ __launch_bounds__(256) void exact_score_kernel(EArgs a, const double*
   if (y >= a.n) return;
   const double nom = sigma_diag<KIND>(a);
   cache[y] = delta_from(nom, qdiag[y], qexact[y] == 1, a.jitter, a.thr);
+}
+
+// ---- pre-tightening (vgposp_exact_pretighten) -----------------------------------------------
+// With two bound levels, every candidate starts on its K_lo-step bound, and any of them that
+// reaches the arg-max during the rounds costs a refinement event (a host round trip, the stall
+// kernel) to be tightened.  Those are the candidates at the top of the round-0 cache, so the M
+// best (by their upper bound of delta) are tightened at once before the rounds: a three-pass
+// radix select of the M-th largest key code (12-bit digits of key_enc's value code, bits 63..28:
+// a bin is then 2^-24 of the value wide), the candidates at or above it listed, their K_hi
+// bounds (the LIST bounds kernel), their round-0 entries re-scored, and the arg-max keys rebuilt.
+// If ties at the threshold would list more than PT_MAX candidates, none is listed (the run then
+// tightens on demand only): the set is never cut by the order of the list's atomics.
+
+constexpr int PT_PASSES = 3;  // digits at bits 63..52, 51..40, 39..28 of the value code
+__device__ __forceinline__ int pt_shift(int pass) { return 52 - 12 * pass; }
+
+// Histogram of the digit at `shift` of the value codes of the candidates still on their first
+// bound whose code matches `prefix` above the digit (pass 0: every such candidate).
+__global__ __launch_bounds__(256) void exact_pt_hist_kernel(const double* cache,
+                                                            const unsigned char* qexact,
+                                                            long long n, const long long* state,
+                                                            int pass, unsigned* hist) {
+  __shared__ unsigned h[PT_BINS];
+  for (int b = threadIdx.x; b < PT_BINS; b += 256) h[b] = 0;
+  __syncthreads();
+  const int shift = pt_shift(pass);
+  const unsigned long long prefix = pass == 0 ? 0ull : (unsigned long long)state[0];
+  const unsigned long long pmask = pass == 0 ? 0ull : ~((1ull << (shift + 12)) - 1);
+  for (long long y = (long long)blockIdx.x * 256 + threadIdx.x; y < n;
+       y += (long long)gridDim.x * 256) {
+    if (qexact[y] != 0) continue;
+    const unsigned long long c = key_enc(cache[y], y).v;
+    if ((c & pmask) == prefix) atomicAdd(&h[(c >> shift) & (PT_BINS - 1)], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < PT_BINS; b += 256)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// The digit of pass `pass`: walking the bins from the top, the one where the count of codes at
+// or above it reaches the candidates still needed; state[0] gets the code prefix, state[1] the
+// need left below the digits above it.  The histogram is cleared for the next pass.  One wave.
+__global__ __launch_bounds__(64) void exact_pt_pick_kernel(long long* state, int pass,
+                                                           unsigned* hist) {
+  if (threadIdx.x == 0) {
+    const int shift = pt_shift(pass);
+    long long need = state[1], cum = 0;
+    int d = 0;
+    for (int b = PT_BINS - 1; b >= 0; --b) {
+      if (cum + hist[b] >= need) {
+        d = b;
+        break;
+      }
+      cum += hist[b];
+    }
+    state[0] = (long long)((unsigned long long)state[0] | ((unsigned long long)d << shift));
+    state[1] = need - cum;
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < PT_BINS; b += 64) hist[b] = 0;
+}
+
+// List the candidates on their first bound with a code >= the threshold (at most PT_MAX; the
+// order of the list does not matter: each candidate's bound is its own).
+__global__ __launch_bounds__(256) void exact_pt_list_kernel(const double* cache,
+                                                            const unsigned char* qexact,
+                                                            long long n, long long* state,
+                                                            long long* list, int* count) {
+  const unsigned long long thr = (unsigned long long)state[0];
+  for (long long y = (long long)blockIdx.x * 256 + threadIdx.x; y < n;
+       y += (long long)gridDim.x * 256) {
+    if (qexact[y] != 0 || key_enc(cache[y], y).v < thr) continue;
+    const unsigned long long i = atomicAdd((unsigned long long*)&state[3], 1ull);
+    if (i < (unsigned long long)PT_MAX) list[i] = y;
+  }
+  (void)count;
+}
+
+__global__ void exact_pt_init_kernel(long long* state, long long M) {
+  if (threadIdx.x == 0) {
+    state[0] = 0;
+    state[1] = M;
+    state[2] = 0;
+    state[3] = 0;
+  }
+}
+
+__global__ void exact_pt_count_kernel(const long long* state, int* count, int* ctl) {
+  if (threadIdx.x == 0) {
+    const int c = state[3] <= PT_MAX ? (int)state[3] : 0;
+    count[0] = c;
+    ctl[CTL_TIGHT] += c;
+  }
+}
+
+// Round-0 entries of the listed candidates from their tightened bounds; qexact <- 2.
+template <int KIND>
+__global__ __launch_bounds__(256) void exact_pt_score_kernel(EArgs a, const double* qdiag,
+                                                             unsigned char* qexact, double* cache,
+                                                             const long long* list,
+                                                             const int* count) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= *count) return;
+  const long long y = list[i];
+  cache[y] = delta_from(sigma_diag<KIND>(a), qdiag[y], false, a.jitter, a.thr);
+  qexact[y] = 2;
 }
 
 // One wave: key of block b (entries [b EB, (b+1) EB) of the cache, selected ones excluded).
@@ -1062,9 +1180,12 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
   constexpr int NW = SEL_THREADS / 64;
   double v[P];
   long long id[P];
+  // items interleaved over the waves (wave w holds items = w mod NW): the best entries of a block
+  // are neighbours in the grid and would otherwise share a wave and force the second pass
+  const int tw = (t & 63) * NW + wave;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    const int i = t + p * SEL_THREADS;
+    const int i = tw + p * SEL_THREADS;
     v[p] = 0.0;
     id[p] = -1;
     if (i < count) key(i, v[p], id[p]);
@@ -2318,6 +2439,66 @@ extern "C" int vgposp_exact_tighten_pending(VGPOSP_EXACT_PARAMS, const int* tab_
     hipLaunchKernelGGL(exact_tighten_end_kernel<decltype(KK)::value>, dim3(1), dim3(SEL_THREADS), 0, s,
                        a, qdiag, cache, selected, w, nblk,
                        reinterpret_cast<const long long*>(picks));
+    VG_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+extern "C" int vgposp_exact_pretighten(VGPOSP_EXACT_PARAMS, const int* tab_off,
+                                       const int* tab_nb, const int* tab_cnt, int T, int K,
+                                       double hi_scale, double mu, int64_t M, void* stream) {
+  VGPOSP_EXACT_PROLOGUE("vgposp_exact_pretighten");
+  VG_CHECK_ARG(tab_off != nullptr && tab_nb != nullptr && tab_cnt != nullptr, 24);
+  VG_CHECK_ARG(T >= 1 && T <= BND_TMAX && (int64_t)T * (m - 1) <= BND_NBMAX, 27);
+  VG_CHECK_ARG(K >= 1 && K <= 4 * BND_SMAX, 28);
+  VG_CHECK_ARG(hi_scale >= 1.0, 29);
+  VG_CHECK_ARG(mu >= 0.0, 30);
+  VG_CHECK_ARG(M >= 1 && M <= PT_MAX / 2, 31);
+  VG_CHECK_ARG(a.m1 == 6, 12);  // the register bounds kernel (the 7-point taper)
+  VG_CHECK_ARG(a.n < (1LL << 31), 3);
+  const long long n = a.n, nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
+  const unsigned sweep = (unsigned)std::min<long long>(ceil_div(n, 256), 2048);
+  double* out = const_cast<double*>(qdiag);
+  ProfScope ps("exact_pretighten", s, 0.0, 0.0);
+  VG_HIP(vg_memset(w.pt_hist, 0, 4 * (size_t)PT_BINS, s));
+  hipLaunchKernelGGL(exact_pt_init_kernel, dim3(1), dim3(64), 0, s, w.pt_state, (long long)M);
+  VG_LAUNCH_CHECK();
+  for (int pass = 0; pass < PT_PASSES; ++pass) {
+    hipLaunchKernelGGL(exact_pt_hist_kernel, dim3(sweep), dim3(256), 0, s, cache, w.qexact, n,
+                       w.pt_state, pass, w.pt_hist);
+    VG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(exact_pt_pick_kernel, dim3(1), dim3(64), 0, s, w.pt_state, pass, w.pt_hist);
+    VG_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(exact_pt_list_kernel, dim3(sweep), dim3(256), 0, s, cache, w.qexact, n,
+                     w.pt_state, w.pt_list, w.pt_count);
+  VG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(exact_pt_count_kernel, dim3(1), dim3(64), 0, s, w.pt_state, w.pt_count,
+                     w.ctl);
+  VG_LAUNCH_CHECK();
+  const unsigned blocks = (unsigned)std::min<long long>(ceil_div(M + 4096, BND_WAVES), 2048);
+#define VG_PT_REG(SMV)                                                                           \
+  if (T <= 64 * SMV) {                                                                           \
+    hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6, true>), dim3(blocks), dim3(BND_T), 0, s,   \
+                       w.coef, a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu,    \
+                       0LL, 0LL, out, w.pt_list, w.pt_count);                                     \
+  } else
+  VG_PT_REG(4) VG_PT_REG(6) VG_PT_REG(9) VG_PT_REG(14) {
+    set_error("vgposp_exact_pretighten: reach table of %d nodes", T);
+    return 27;
+  }
+#undef VG_PT_REG
+  VG_LAUNCH_CHECK();
+  return dispatch_kind(kind, [&](auto KK) {
+    hipLaunchKernelGGL(exact_pt_score_kernel<decltype(KK)::value>,
+                       dim3((unsigned)ceil_div(PT_MAX, 256)), dim3(256), 0, s, a, qdiag, w.qexact,
+                       cache, w.pt_list, w.pt_count);
+    VG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(exact_block_keys_kernel, dim3((unsigned)ceil_div(nblk, 4)), dim3(256), 0, s,
+                       cache, selected, n, w.bval, w.bidx, nblk);
+    VG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(exact_super_keys_kernel, dim3((unsigned)ceil_div(nsb, 4)), dim3(256), 0, s,
+                       w.bval, w.bidx, nblk, w.sval, w.sidx, nsb);
     VG_LAUNCH_CHECK();
     return 0;
   });

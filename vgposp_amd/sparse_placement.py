@@ -416,6 +416,7 @@ BOUND_MARGIN = 1e-12                       # relative rounding margin on the upp
 # (width <= BOUND_HI_TARGET, K = 6) before any of them is given a CG column.  One K = 5 level for
 # all (round 3's) cost the 2M-candidate bounds pass 4.8 ms at 128^3.
 BOUND_LO_TARGET = 3e-5
+PRETIGHTEN = 4096      # two levels: candidates tightened before the rounds (at most 32,768)
 BOUND_HI_TARGET = 1e-7
 
 
@@ -480,14 +481,18 @@ class ExactWindowGreedy:
         self.refine_batches = 0   # batched CG solves in the last bounded run
         self.bound = None
         self.tight = None
-        # bound_qdiag's default: ONE bound level.  With the Gauss-Radau bounds one level of K = 4
-        # steps (bracket ~9e-7) runs the 128^3 k = 50 case in 7.3 ms against 8.7 ms for two
-        # levels (K = 3 for all, K = 5 before a CG column): the second level's extra refinement
-        # events (6 host round trips and top-B selections instead of 3) cost more than its
-        # cheaper first pass saves (profiles/r4_c4_radau.jsonl)
-        self.two_level = False
+        # bound_qdiag's default: two bound levels (Gauss-Radau K = 3 for every candidate, K = 5
+        # for the `pretighten` best round-0 entries at once and for any other that reaches a
+        # refinement batch): 6.2 ms per 128^3 k = 50 run against 6.8 for one level of K = 4.
+        # Without the pre-tightening two levels lost (8.0 ms: 134 candidates tightened in 6
+        # refinement events, each a host round trip; profiles/r4_c4_pretighten.jsonl)
+        self.two_level = True
         self.radau = True         # Gauss-Radau upper bounds (mu = the Gershgorin lambda_min)
         self.bound_target = 1e-6  # one-level bracket target (Chebyshev width; Radau: one step less)
+        self.lo_target = BOUND_LO_TARGET  # two levels: the first level's bracket target
+        # two levels: the candidates with the largest round-0 entries tightened at once before
+        # the rounds (vgposp_exact_pretighten); 0 = only on demand, by refinement events
+        self.pretighten = PRETIGHTEN
         self.bound_mu = 0.0       # mu of the last bounds (0: the Chebyshev bound)
         self.tightened = 0        # candidates tightened to the K_hi bound in the last bounded run
 
@@ -540,7 +545,7 @@ class ExactWindowGreedy:
         if steps is not None:
             b = steps
         else:
-            b = bound_steps(offs, lo, hi, target=BOUND_LO_TARGET if two else self.bound_target)
+            b = bound_steps(offs, lo, hi, target=self.lo_target if two else self.bound_target)
         self.tight = None
         self.bound_mu = float(mu) if steps is not None else 0.0
         if b is None:
@@ -614,6 +619,8 @@ class ExactWindowGreedy:
         if tight is not None:
             ttab, tT = self._device_table(tight[0])
             targs = (*[_p(a) for a in ttab], tT, tight[0], tight[1], self.bound_mu, pk)
+        if tight is not None and self.pretighten > 0:
+            call("vgposp_exact_pretighten", *args, *targs[:-1], int(self.pretighten), st)
         call("vgposp_exact_steps", *args, 0, 1, k, B, pk, pd, st)  # round 0 stalls: nothing refined
         issued, reads = 1, 0
         while True:
