@@ -416,7 +416,7 @@ BOUND_MARGIN = 1e-12                       # relative rounding margin on the upp
 # (width <= BOUND_HI_TARGET, K = 6) before any of them is given a CG column.  One K = 5 level for
 # all (round 3's) cost the 2M-candidate bounds pass 4.8 ms at 128^3.
 BOUND_LO_TARGET = 3e-5
-PRETIGHTEN = 4096      # two levels: candidates tightened before the rounds (at most 32,768)
+PRETIGHTEN = 2048      # two levels: candidates tightened before the rounds (at most 32,768)
 BOUND_HI_TARGET = 1e-7
 
 
@@ -482,8 +482,8 @@ class ExactWindowGreedy:
         self.bound = None
         self.tight = None
         # bound_qdiag's default: two bound levels (Gauss-Radau K = 3 for every candidate, K = 5
-        # for the `pretighten` best round-0 entries at once and for any other that reaches a
-        # refinement batch): 6.2 ms per 128^3 k = 50 run against 6.8 for one level of K = 4.
+        # for the `pretighten` (2,048) best round-0 entries at once and for any other that reaches a
+        # refinement batch): 6.3 ms per 128^3 k = 50 run against 6.75 for one level of K = 4.
         # Without the pre-tightening two levels lost (8.0 ms: 134 candidates tightened in 6
         # refinement events, each a host round trip; profiles/r4_c4_pretighten.jsonl)
         self.two_level = True
