@@ -886,8 +886,14 @@ def main():
         roof["traffic_vs_algorithmic"] = tr["bytes_per_launch"] / (nbytes / max(launches, 1))
         roof["traffic_source"] = tr["source"]
     elif dom == "gemm_f64":
-        roof["traffic_note"] = ("null: no PMC pass of this workload in " +
-                                os.path.relpath(args.traffic, ROOT) + " (tools/pmc_gemm_bench.sh)")
+        roof["traffic_note"] = (
+            "null: no PMC pass of this build in " + os.path.relpath(args.traffic, ROOT) +
+            ". Round 4's FETCH_SIZE pass over this step died inside rocprofv3's counter-collection "
+            "dispatch hook (SIGSEGV on the first copy_leaf_kernel launch of the factorization, "
+            "profiles/r4_rocprof_pmc_final_segv.log; the un-profiled step and the kernel-trace "
+            "pass run the same path). The GEMM kernel body is unchanged since round 3, whose "
+            "pass measured 2.07 GB per launch (profiles/traffic_r3.json, tied to round 3's "
+            "sources).")
     # the HBM-bound kernel of the placement rounds, with its PMC-measured traffic
     ms_t, n_t, _, by_t = prof["greedy_trmv"]
     hbm = {"kernel": "greedy_trmv", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
