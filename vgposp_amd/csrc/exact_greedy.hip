@@ -330,6 +330,9 @@ __device__ __forceinline__ double bound_value(double g, double gmu, double rrK, 
   return mu > 0.0 ? hi_scale * fma(gmu, rrK, g) : hi_scale * g;
 }
 
+#ifndef VGPOSP_BND_GRID  // (A/B: workgroups of the all-candidate bounds launch, at most)
+#define VGPOSP_BND_GRID 65536
+#endif
 constexpr int BND_T = 256;
 constexpr int BND_WAVES = BND_T / 64;
 constexpr int BND_SMAX = 14;
@@ -651,25 +654,56 @@ __global__ __launch_bounds__(256) void exact_pt_hist_kernel(const double* cache,
 
 // The digit of pass `pass`: walking the bins from the top, the one where the count of codes at
 // or above it reaches the candidates still needed; state[0] gets the code prefix, state[1] the
-// need left below the digits above it.  The histogram is cleared for the next pass.  One wave.
+// need left below the digits above it.  The histogram is cleared for the next pass.  One wave:
+// the bins staged in LDS, lane l sums the l-th chunk of 64 from the top, a scan over the lanes
+// finds the chunk, and its lane walks it (one thread walking the 4,096 bins in global memory
+// took 143 us).
 __global__ __launch_bounds__(64) void exact_pt_pick_kernel(long long* state, int pass,
                                                            unsigned* hist) {
-  if (threadIdx.x == 0) {
-    const int shift = pt_shift(pass);
-    long long need = state[1], cum = 0;
-    int d = 0;
-    for (int b = PT_BINS - 1; b >= 0; --b) {
-      if (cum + hist[b] >= need) {
-        d = b;
+  __shared__ unsigned h[PT_BINS];
+  __shared__ long long s_res[2];
+  const int lane = threadIdx.x;
+  for (int b = lane; b < PT_BINS; b += 64) h[b] = hist[b];
+  __syncthreads();
+  constexpr int CH = PT_BINS / 64;
+  const int top = PT_BINS - 1 - CH * lane;  // this lane's chunk: bins top .. top - CH + 1
+  unsigned cs = 0;
+  for (int j = 0; j < CH; ++j) cs += h[top - j];
+  const long long need = state[1];
+  // inclusive prefix of the chunk sums from the top chunk (lane 0) down
+  long long incl = cs;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const unsigned long long hit = __ballot(incl >= need);
+  if (hit == 0ull) {  // fewer candidates than needed: everything from digit 0 up
+    if (lane == 63) {
+      s_res[0] = 0;
+      s_res[1] = incl;
+    }
+  } else if (lane == __ffsll((long long)hit) - 1) {
+    long long cum = incl - cs;
+    int d = top - CH + 1;
+    for (int j = 0; j < CH; ++j) {
+      if (cum + h[top - j] >= need) {
+        d = top - j;
         break;
       }
-      cum += hist[b];
+      cum += h[top - j];
     }
-    state[0] = (long long)((unsigned long long)state[0] | ((unsigned long long)d << shift));
-    state[1] = need - cum;
+    s_res[0] = d;
+    s_res[1] = cum;
   }
   __syncthreads();
-  for (int b = threadIdx.x; b < PT_BINS; b += 64) hist[b] = 0;
+  if (lane == 0) {
+    const int shift = pt_shift(pass);
+    state[0] = (long long)((unsigned long long)state[0] |
+                           ((unsigned long long)s_res[0] << shift));
+    state[1] = need - s_res[1];
+  }
+  for (int b = lane; b < PT_BINS; b += 64) hist[b] = 0;
 }
 
 // List the candidates on their first bound with a code >= the threshold (at most PT_MAX; the
@@ -1448,10 +1482,15 @@ __device__ __forceinline__ double qcol_staged(const ExactWS& w, const StagedPick
 // s_yy - |LS^-1 s_Ay|^2, P = qyy - |LQ^-1 q_Ay|^2.  Lane s holds the forward-substitution
 // unknowns z_s and z_{s+64}; every lane returns the delta.  sp: the picks staged in LDS
 // (stage_picks) or nullptr (read from the workspace).
+// The right-hand sides of a re-score: lane s holds s_{a_s y} and q_{a_s y} (and s + 64's).
+struct RescoreVals {
+  double vs0, vq0, vs1, vq1;
+};
+
 template <int KIND>
-__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRows& L,
-                               const long long* picks, int nA, long long y, double qyy,
-                               bool exact, const StagedPicks* sp = nullptr) {
+__device__ __forceinline__ RescoreVals wave_rescore_vals(const EArgs& a, const ExactWS& w,
+                                                         const long long* picks, int nA,
+                                                         long long y, const StagedPicks* sp) {
   const int lane = threadIdx.x & 63;
   double vs0 = 0.0, vq0 = 0.0, vs1 = 0.0, vq1 = 0.0;
   if (sp) {
@@ -1474,6 +1513,15 @@ __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRow
       vq1 = qcol_at(w, lane + 64, y, a.I1, a.I2);
     }
   }
+  return RescoreVals{vs0, vq0, vs1, vq1};
+}
+
+// The forward substitutions of a re-score from its right-hand sides (rows 0 .. nA - 1 of L).
+template <int KIND>
+__device__ double wave_rescore_subst(const EArgs& a, const FactorRows& L, int nA, double qyy,
+                                     bool exact, const RescoreVals& v) {
+  const int lane = threadIdx.x & 63;
+  const double vs0 = v.vs0, vq0 = v.vq0, vs1 = v.vs1, vq1 = v.vq1;
   double zs0 = 0.0, zq0 = 0.0, zs1 = 0.0, zq1 = 0.0;
   for (int r = 0; r < nA; ++r) {
     double ds = 0.0, dq = 0.0;
@@ -1501,6 +1549,14 @@ __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRow
   const double ns = wave_sum(fma(zs0, zs0, zs1 * zs1));
   const double nq = wave_sum(fma(zq0, zq0, zq1 * zq1));
   return delta_from(sigma_diag<KIND>(a) - ns, qyy - nq, exact, a.jitter, a.thr);
+}
+
+template <int KIND>
+__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRows& L,
+                               const long long* picks, int nA, long long y, double qyy,
+                               bool exact, const StagedPicks* sp = nullptr) {
+  const RescoreVals v = wave_rescore_vals<KIND>(a, w, picks, nA, y, sp);
+  return wave_rescore_subst<KIND>(a, L, nA, qyy, exact, v);
 }
 
 // Bounded-lazy path, after the CG columns of the batch (cands[j] in slots[j], j < nb): each Q_cc
@@ -1695,18 +1751,30 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
   const bool lds = nr * (nr + 1) <= ROWS_LDS;
   const FactorRows L = lds ? stage_rows(w, a.kmax, round, sm)
                            : (__syncthreads(), global_rows(w, a.kmax));
+  // the candidate's right-hand sides need only the staged picks: loaded before the new row (whose
+  // chain they then overlap), the substitutions after it
+  const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const bool live = e < v.w0 * v.w1 * v.w2;
+  const long long y = live ? ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) *
+                                     a.I2 + v.lo2 + e % v.w2
+                           : 0;
+  const bool picked = live && sel[y];
+  RescoreVals rv{0.0, 0.0, 0.0, 0.0};
+  double qyy = 0.0;
+  bool ex = false;
+  if (live && !picked) {
+    rv = wave_rescore_vals<KIND>(a, w, picks, nr, y, &sp);
+    qyy = qdiag[y];
+    ex = w.qexact[y] == 1;
+  }
   if ((threadIdx.x >> 6) < 2) wave_new_row<KIND>(a, w, round, L, sp, lds ? sm : nullptr);
   __syncthreads();
-  const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (e >= v.w0 * v.w1 * v.w2) return;
-  const long long y = ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) * a.I2 +
-                      v.lo2 + e % v.w2;
-  if (sel[y]) {
+  if (!live) return;
+  if (picked) {
     if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
     return;
   }
-  const double d = wave_rescore<KIND>(a, w, L, picks, round + 1, y, qdiag[y], w.qexact[y] == 1,
-                                      &sp);
+  const double d = wave_rescore_subst<KIND>(a, L, nr, qyy, ex, rv);
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
@@ -2289,7 +2357,8 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   ProfScope ps("exact_bounds", s, 0.0, 0.0);
   const long long waves = c1 - c0;
   const unsigned blocks =
-      (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES), 8LL), 8192));
+      (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES), 8LL),
+                                         VGPOSP_BND_GRID / 8));
   double* out = const_cast<double*>(qdiag);
   const long long lc0 = c0, lc1 = c1;
 #define VG_BOUNDS_REG(SMV)                                                                       \
