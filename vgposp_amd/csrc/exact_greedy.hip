@@ -450,6 +450,90 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
 #else
 #define VG_BND_ATTR
 #endif
+// A coefficient row (M doubles of the 16-byte-aligned padded row gi, zeros for gi < 0) in
+// two-double loads.
+template <int M>
+__device__ __forceinline__ void load_coef_row(const double* __restrict__ coef, int gi, double* c) {
+  constexpr int MS = coef_stride(M);
+#pragma unroll
+  for (int o = 0; o < MS; o += 2) {
+    double2 v = make_double2(0.0, 0.0);
+    if (gi >= 0) v = *reinterpret_cast<const double2*>(coef + (size_t)gi * MS + o);
+    if (o < M) c[o] = v.x;
+    if (o + 1 < M) c[o + 1] = v.y;
+  }
+}
+
+// K CG steps on (Sigma + eps I) x = e_y from x = 0 with the candidate's coefficient rows c (slot s
+// on lane s * 64 + lane, node 0 = y) and the lanes' neighbour byte offsets nbo into the wave's LDS
+// vector pl: the upper bound of Q_yy (bound_value), on every lane.
+template <int SM, int M1>
+__device__ __forceinline__ double bounds_cg(const double (&c)[SM][M1 + 1],
+                                            const unsigned (&nbo)[SM][(M1 + 1) / 2], double* pl,
+                                            const int* cntl, int K, double hi_scale, double mu,
+                                            int lane) {
+  const char* plb = reinterpret_cast<const char*>(pl);
+  double r[SM], p[SM], q[SM];
+#pragma unroll
+  for (int s = 0; s < SM; ++s) {
+    const int j = s * 64 + lane;
+    r[s] = (j == 0) ? 1.0 : 0.0;
+    p[s] = r[s];
+    pl[j] = r[s];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double rr = 1.0, g = 0.0, gmu = mu > 0.0 ? 1.0 / mu : 0.0;
+  for (int it = 0; it < K; ++it) {
+    const int cnt = cntl[it + 1];
+    double pq = 0.0;
+#pragma unroll
+    for (int s = 0; s < SM; ++s) {
+      q[s] = 0.0;
+      if (s * 64 < cnt) {
+        const int j = s * 64 + lane;
+        double acc = c[s][0] * p[s];
+#pragma unroll
+        for (int o = 0; o < M1; ++o) {
+          const unsigned off = (nbo[s][o >> 1] >> (16 * (o & 1))) & 0xffffu;
+          acc = fma(c[s][1 + o], *reinterpret_cast<const double*>(plb + off), acc);
+        }
+        q[s] = j < cnt ? acc : 0.0;
+        pq = fma(p[s], q[s], pq);
+      }
+    }
+    pq = wave_sum(pq);
+    const double alpha = rr / pq;
+    g = fma(alpha, rr, g);
+    if (it + 1 == K && mu <= 0.0) break;
+    double rn = 0.0;
+#pragma unroll
+    for (int s = 0; s < SM; ++s) {
+      r[s] = fma(-alpha, q[s], r[s]);
+      rn = fma(r[s], r[s], rn);
+    }
+    rn = wave_sum(rn);
+    if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, rn / rr);
+    const double beta = rn / rr;
+    rr = rn;
+    if (it + 1 == K) break;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s = 0; s < SM; ++s) {
+      p[s] = fma(beta, p[s], r[s]);
+      if (s * 64 < cnt) pl[s * 64 + lane] = p[s];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // (the last step's pl reads fed wave_sum, so the next candidate's pl writes cannot pass them)
+  return bound_value(g, gmu, rr, mu, hi_scale);
+}
+
 template <int SM, int M1, bool LIST = false>
 __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
@@ -486,7 +570,6 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
       const unsigned hi = 2 * o + 1 < M1 ? 8u * (unsigned)nbl[j * M1 + 2 * o + 1] : 0u;
       nbo[s][o] = lo | (hi << 16);
     }
-  const char* plb = reinterpret_cast<const char*>(pl);
   // the lane's table offsets, likewise once: three signed bytes per slot (|offset| <= K <= 56)
   int ofr[SM];
 #pragma unroll
@@ -523,10 +606,8 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
     const int y0 = (int)(yu / I12), yr = (int)(yu - (unsigned)y0 * I12);
     const int y1 = yr / I2i, y2 = yr - y1 * I2i;
     double c[SM][M];
-    double r[SM], p[SM], q[SM];
 #pragma unroll
     for (int s = 0; s < SM; ++s) {
-      const int j = s * 64 + lane;
       int gi = -1;
       if (ofr[s] >= 0) {
         const int g0 = y0 + (ofr[s] & 255) - 128, g1 = y1 + ((ofr[s] >> 8) & 255) - 128,
@@ -535,71 +616,102 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
             (unsigned)g2 < (unsigned)I2i)
           gi = (g0 * I1i + g1) * I2i + g2;
       }
-      // the padded row in two-double loads
-      constexpr int MS = coef_stride(M);
-#pragma unroll
-      for (int o = 0; o < MS; o += 2) {
-        double2 v = make_double2(0.0, 0.0);
-        if (gi >= 0) v = *reinterpret_cast<const double2*>(coef + (size_t)gi * MS + o);
-        if (o < M) c[s][o] = v.x;
-        if (o + 1 < M) c[s][o + 1] = v.y;
-      }
-      r[s] = (j == 0) ? 1.0 : 0.0;
-      p[s] = r[s];
-      pl[j] = r[s];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double rr = 1.0, g = 0.0, gmu = mu > 0.0 ? 1.0 / mu : 0.0;
-    for (int it = 0; it < K; ++it) {
-      const int cnt = cntl[it + 1];
-      double pq = 0.0;
-#pragma unroll
-      for (int s = 0; s < SM; ++s) {
-        q[s] = 0.0;
-        if (s * 64 < cnt) {
-          const int j = s * 64 + lane;
-          double acc = c[s][0] * p[s];
-#pragma unroll
-          for (int o = 0; o < M1; ++o) {
-            const unsigned off = (nbo[s][o >> 1] >> (16 * (o & 1))) & 0xffffu;
-            acc = fma(c[s][1 + o], *reinterpret_cast<const double*>(plb + off), acc);
-          }
-          q[s] = j < cnt ? acc : 0.0;
-          pq = fma(p[s], q[s], pq);
-        }
-      }
-      pq = wave_sum(pq);
-      const double alpha = rr / pq;
-      g = fma(alpha, rr, g);
-      if (it + 1 == K && mu <= 0.0) break;
-      double rn = 0.0;
-#pragma unroll
-      for (int s = 0; s < SM; ++s) {
-        r[s] = fma(-alpha, q[s], r[s]);
-        rn = fma(r[s], r[s], rn);
-      }
-      rn = wave_sum(rn);
-      if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, rn / rr);
-      const double beta = rn / rr;
-      rr = rn;
-      if (it + 1 == K) break;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int s = 0; s < SM; ++s) {
-        p[s] = fma(beta, p[s], r[s]);
-        if (s * 64 < cnt) pl[s * 64 + lane] = p[s];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      load_coef_row<M>(coef, gi, c[s]);
     }
     // (LIST: both bounds are valid, the smaller one is kept)
-    const double ub = bound_value(g, gmu, rr, mu, hi_scale);
+    const double ub = bounds_cg<SM, M1>(c, nbo, pl, cntl, K, hi_scale, mu, lane);
     if (lane == 0) qhi[y] = LIST ? fmin(qhi[y], ub) : ub;
+  }
+}
+
+// The all-candidate bounds for K <= BT_H steps on the 7-point stencil (one reach-table slot per
+// lane, T <= 64), tiled: a workgroup takes a BT_E^3 tile of candidates and stages the coefficient
+// rows of the tile and its BT_H halo (BT_B^3 = 1,000 rows, 56 KB as seven planes) into LDS once,
+// with neighbouring rows on neighbouring lanes; a candidate's 63 rows are then LDS reads, not 63
+// scattered 64-byte global loads (15.6 staged rows per candidate against 63 loaded ones).  The CG
+// is exactly exact_bounds_reg_kernel's (bounds_cg, the same coefficients in the same order), so
+// the bounds are bit-identical.  A table offset outside the halo (a stencil with longer reach)
+// reads its row from global memory, as the register kernel does.
+// A/B only (-DVGPOSP_BND_TILE=1, profiles/r4_c4_bounds_tile.jsonl): bounds bit-identical, but the
+// 128^3 K = 3 pass takes 1.81 ms against the register kernel's 1.70.  The coefficient loads were
+// not the bound: a candidate is ~500 wave instructions of CG (the six gathers, FMAs, two wave
+// sums and three fp64 divisions per step), and the 61 KB of LDS halves the waves per SIMD.
+constexpr int BT_E = 4, BT_H = 3, BT_B = BT_E + 2 * BT_H, BT_ROWS = BT_B * BT_B * BT_B;
+constexpr int BT_T = 512, BT_WAVES = BT_T / 64;
+
+template <int M1>
+__global__ __launch_bounds__(BT_T) void exact_bounds_tile_kernel(
+    const double* __restrict__ coef, long long I0, long long I1, long long I2,
+    const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
+    const int* __restrict__ tab_cnt, int T, int K, double hi_scale, double mu, long long c0,
+    long long c1, double* __restrict__ qhi, int tile_lo, int tile_hi, int per_xcd) {
+  constexpr int M = M1 + 1;
+  __shared__ double cl[M][BT_ROWS];
+  __shared__ double plds[BT_WAVES][64 + 1];
+  __shared__ short nbl[64 * M1];
+  __shared__ int cntl[4 * BND_SMAX + 1];
+  // XCD-aware: XCD x (= blockIdx.x mod 8) takes its own contiguous run of tiles, so the halos
+  // neighbouring tiles share meet in the same L2
+  const int tile = tile_lo + (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+  if (tile >= tile_hi) return;  // (whole workgroup)
+  const int I0i = (int)I0, I1i = (int)I1, I2i = (int)I2;
+  const int TD1 = (I1i + BT_E - 1) / BT_E, TD2 = (I2i + BT_E - 1) / BT_E;
+  const int t0 = tile / (TD1 * TD2) * BT_E, t1 = tile / TD2 % TD1 * BT_E, t2 = tile % TD2 * BT_E;
+  for (int i = threadIdx.x; i < 64 * M1; i += BT_T) {
+    const int v = i < T * M1 ? tab_nb[i] : -1;
+    nbl[i] = (short)(v >= 0 ? v : 64);
+  }
+  for (int i = threadIdx.x; i <= K; i += BT_T) cntl[i] = tab_cnt[i];
+  for (int b = threadIdx.x; b < BT_ROWS; b += BT_T) {
+    const int g0 = t0 - BT_H + b / (BT_B * BT_B), g1 = t1 - BT_H + b / BT_B % BT_B,
+              g2 = t2 - BT_H + b % BT_B;
+    int gi = -1;
+    if ((unsigned)g0 < (unsigned)I0i && (unsigned)g1 < (unsigned)I1i && (unsigned)g2 < (unsigned)I2i)
+      gi = (g0 * I1i + g1) * I2i + g2;
+    double row[M];
+    load_coef_row<M>(coef, gi, row);
+#pragma unroll
+    for (int o = 0; o < M; ++o) cl[o][b] = row[o];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* pl = plds[wave];
+  if (lane == 0) pl[64] = 0.0;
+  __syncthreads();
+  constexpr int NP = (M1 + 1) / 2;
+  unsigned nbo[1][NP];
+#pragma unroll
+  for (int o = 0; o < NP; ++o) {
+    const unsigned lo = 8u * (unsigned)nbl[lane * M1 + 2 * o];
+    const unsigned hi = 2 * o + 1 < M1 ? 8u * (unsigned)nbl[lane * M1 + 2 * o + 1] : 0u;
+    nbo[0][o] = lo | (hi << 16);
+  }
+  // the lane's node: its offset in the staged box (inbox) or, outside the halo, its grid offset
+  int o0 = 0, o1 = 0, o2 = 0;
+  const bool valid = lane < T;
+  if (valid) o0 = tab_off[3 * lane], o1 = tab_off[3 * lane + 1], o2 = tab_off[3 * lane + 2];
+  const bool inbox = valid && abs(o0) <= BT_H && abs(o1) <= BT_H && abs(o2) <= BT_H;
+  const int dob = (o0 * BT_B + o1) * BT_B + o2;
+  for (int lc = wave; lc < BT_E * BT_E * BT_E; lc += BT_WAVES) {
+    const int l0 = lc / (BT_E * BT_E), l1 = lc / BT_E % BT_E, l2 = lc % BT_E;
+    const int y0 = t0 + l0, y1 = t1 + l1, y2 = t2 + l2;
+    if (y0 >= I0i || y1 >= I1i || y2 >= I2i) continue;  // (whole wave)
+    const long long y = ((long long)y0 * I1i + y1) * I2i + y2;
+    if (y < c0 || y >= c1) continue;
+    double c[1][M];
+    if (inbox) {
+      const int b = ((l0 + BT_H) * BT_B + (l1 + BT_H)) * BT_B + (l2 + BT_H) + dob;
+#pragma unroll
+      for (int o = 0; o < M; ++o) c[0][o] = cl[o][b];
+    } else {
+      int gi = -1;
+      const int g0 = y0 + o0, g1 = y1 + o1, g2 = y2 + o2;
+      if (valid && (unsigned)g0 < (unsigned)I0i && (unsigned)g1 < (unsigned)I1i &&
+          (unsigned)g2 < (unsigned)I2i)
+        gi = (g0 * I1i + g1) * I2i + g2;
+      load_coef_row<M>(coef, gi, c[0]);
+    }
+    const double ub = bounds_cg<1, M1>(c, nbo, pl, cntl, K, hi_scale, mu, lane);
+    if (lane == 0) qhi[y] = ub;
   }
 }
 
@@ -2361,7 +2473,22 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
                                          VGPOSP_BND_GRID / 8));
   double* out = const_cast<double*>(qdiag);
   const long long lc0 = c0, lc1 = c1;
-#define VG_BOUNDS_REG(SMV)                                                                       \
+#ifndef VGPOSP_BND_TILE  // (A/B: 1 = the tiled kernel for T <= 64; measured slower, see there)
+#define VGPOSP_BND_TILE 0
+#endif
+  if (VGPOSP_BND_TILE && a.m1 == 6 && T <= 64) {
+    // the tiles of the grid planes y0 that [c0, c1) touches
+    const long long plane = a.I1 * a.I2;
+    const long long TD1 = ceil_div(a.I1, (long long)BT_E), TD2 = ceil_div(a.I2, (long long)BT_E);
+    const long long lo = c0 / plane / BT_E * TD1 * TD2, hi = ((c1 - 1) / plane / BT_E + 1) * TD1 * TD2;
+    const long long per_xcd = ceil_div(hi - lo, 8LL);
+    hipLaunchKernelGGL(exact_bounds_tile_kernel<6>, dim3((unsigned)(8 * per_xcd)), dim3(BT_T), 0, s,
+                       w.coef, a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0,
+                       lc1, out, (int)lo, (int)hi, (int)per_xcd);
+    VG_LAUNCH_CHECK();
+    return 0;
+  }
+#define VG_BOUNDS_REG(SMV)                                                                     \
   if (T <= 64 * SMV) {                                                                           \
     hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6>), dim3(blocks), dim3(BND_T), 0, s, w.coef, \
                        a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0, lc1,   \
