@@ -81,7 +81,9 @@ __device__ __forceinline__ void xor_pair32(unsigned x, unsigned& a, unsigned& b)
     constexpr int CTRL = O == 8 ? 0x128 : O == 4 ? 0x124 : O == 2 ? 0x4E : 0xB1;
     static_assert(O == 8 || O == 4 || O == 2 || O == 1, "butterfly step");
     a = x;
-    b = (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+    // (every lane reads a valid source under these controls with all rows and banks enabled, so
+    // the mov has no old value to preserve: no zero-initialised destination per step)
+    b = (unsigned)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
   }
 }
 

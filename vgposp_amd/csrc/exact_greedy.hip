@@ -514,8 +514,9 @@ __device__ __forceinline__ double bounds_cg(const double (&c)[SM][M1 + 1],
       rn = fma(r[s], r[s], rn);
     }
     rn = wave_sum(rn);
-    if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, rn / rr);
-    const double beta = rn / rr;
+    // (one division for both: as two, the compiler kept both across the mu branch)
+    const double beta = rn / rr;  // = delta_{k+1}
+    if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, beta);
     rr = rn;
     if (it + 1 == K) break;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
