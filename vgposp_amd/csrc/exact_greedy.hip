@@ -553,7 +553,9 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
   }
   for (int i = threadIdx.x; i < 3 * TP; i += BND_T) offl[i] = (short)(i < 3 * T ? tab_off[i] : 0);
   for (int i = threadIdx.x; i <= K; i += BND_T) cntl[i] = tab_cnt[i];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // (the wave index through readfirstlane: the candidate loop and its index decode are then
+  // wave-uniform scalar work on the SALU instead of VALU slots)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   double* pl = plds[wave];
   if (lane == 0) pl[TP] = 0.0;
   __syncthreads();
