@@ -238,13 +238,11 @@ __device__ __forceinline__ double delta_from(double nom, double P, bool exact, d
   return nom / fmax(den, thr);
 }
 
-// coef[i][0] = S_ii + eps, coef[i][1 + o] = S(i, i + off_o) (0 outside the grid)
+// coef[i][0] = S_ii + eps, coef[i][1 + o] = S(i, i + off_o) (0 outside the grid): row i into c
+// (its padded stride of doubles)
 template <int KIND>
-__global__ __launch_bounds__(256) void exact_coef_kernel(EArgs a, double* __restrict__ coef) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
+__device__ __forceinline__ void coef_row(const EArgs& a, long long i, double* c) {
   const int m = a.m1 + 1;
-  double* c = coef + i * coef_stride(m);
   c[0] = sigma_diag<KIND>(a) + a.jitter;
   if (coef_stride(m) > m) c[m] = 0.0;
   const long long i0 = i / (a.I1 * a.I2), i1 = (i / a.I2) % a.I1, i2 = i % a.I2;
@@ -256,6 +254,29 @@ __global__ __launch_bounds__(256) void exact_coef_kernel(EArgs a, double* __rest
       v = sigma_off<KIND>(a, i, (j0 * a.I1 + j1) * a.I2 + j2);
     c[1 + o] = v;
   }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void exact_coef_kernel(EArgs a, double* __restrict__ coef) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  coef_row<KIND>(a, i, coef + i * coef_stride(a.m1 + 1));
+}
+
+// The same rows for a stride of 8 (the 7-point stencil), written through LDS: a thread's eight
+// 8-byte stores each touch 64 rows of its wave at once, partial lines (WRITE_SIZE read 4.8x the
+// table's 64 bytes per row), so the block's 256 rows are assembled in LDS and stored as one
+// contiguous 16 KB run of 16-byte stores.  The same values in the same places.
+template <int KIND>
+__global__ __launch_bounds__(256) void exact_coef8_kernel(EArgs a, double* __restrict__ coef) {
+  __shared__ double rows[256 * 8];
+  const long long i0 = (long long)blockIdx.x * 256, i = i0 + threadIdx.x;
+  if (i < a.n) coef_row<KIND>(a, i, rows + threadIdx.x * 8);
+  __syncthreads();
+  const int nrow = (int)min(256LL, a.n - i0);
+  double2* dst = reinterpret_cast<double2*>(coef + i0 * 8);
+  const double2* src = reinterpret_cast<const double2*>(rows);
+  for (int k = threadIdx.x; k < nrow * 4; k += 256) dst[k] = src[k];
 }
 
 // Gershgorin bounds of the spectrum of S + eps I from the coefficient table: per row
@@ -2441,8 +2462,12 @@ extern "C" int vgposp_exact_coef(VGPOSP_EXACT_PARAMS, void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_coef");
   const long long n = a.n;
   const int rc = dispatch_kind(kind, [&](auto K) {
-    hipLaunchKernelGGL(exact_coef_kernel<decltype(K)::value>, dim3((unsigned)ceil_div(n, 256)),
-                       dim3(256), 0, s, a, w.coef);
+    if (coef_stride(m) == 8)
+      hipLaunchKernelGGL(exact_coef8_kernel<decltype(K)::value>, dim3((unsigned)ceil_div(n, 256)),
+                         dim3(256), 0, s, a, w.coef);
+    else
+      hipLaunchKernelGGL(exact_coef_kernel<decltype(K)::value>, dim3((unsigned)ceil_div(n, 256)),
+                         dim3(256), 0, s, a, w.coef);
     VG_LAUNCH_CHECK();
     return 0;
   });
