@@ -66,6 +66,8 @@ def parse():
                         "the multi-rank path on one GPU with VGPOSP_BENCH_DEVICE=0)")
     p.add_argument("--c4-pmc", default=os.path.join(ROOT, "profiles", "pmc_c4_r4.json"),
                    help="per-run C4 kernel bytes from rocprofv3 PMC passes (tools/pmc_c4.py)")
+    p.add_argument("--rank-check", action="store_true",
+                   help="(tests) every rank prints its rank / world size and exits before any GPU call")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r4.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
@@ -709,16 +711,51 @@ def splits_line(args, world, barrier, maxtime, rank):
                                    "dense-exact, no collective", "splits": world}}
 
 
+def launch_ranks(args):
+    """``python bench.py --gpus N`` (N > 1) outside a launcher: start the N ranks ourselves.
+
+    The parent makes no GPU call (torch is not even imported here): it runs
+    ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1`` on this
+    same command line as a CHILD process (never an exec), streams the children's stdout through —
+    rank 0 prints the one JSON line — and returns the launcher's exit status, non-zero if any rank
+    failed."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
+    print(f"bench.py: starting {args.gpus} ranks: {' '.join(cmd[1:6])}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    rc = proc.wait()
+    if rc != 0:
+        print(f"bench.py: rank launcher exited with status {rc}", file=sys.stderr, flush=True)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: the ranks must equal --gpus")
+    if args.rank_check:
+        print(json.dumps({"rank": rank, "local_rank": local, "n_gpus": world}), flush=True)
+        return
     # VGPOSP_BENCH_DEVICE pins every rank to one device (rehearsing N > 1 on a one-GPU box)
     dev = int(os.environ.get("VGPOSP_BENCH_DEVICE", local))
     torch.cuda.set_device(dev)

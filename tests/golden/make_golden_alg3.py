@@ -2,7 +2,7 @@
 
 Run in the build container only (``/root/reference`` is absent on the GPU box):
 
-    python tests/golden/make_golden_alg3.py
+    python tests/golden/make_golden_alg3.py [--jobs J] [case ...]
 
 The reference's algorithm 3 (``snippets_a3.sparse_placement_algorithm_3``, snippets_a3.py:43-364)
 is a TF1 graph and TF is absent here.  Its per-delta arithmetic is not TF-specific: with
@@ -62,6 +62,10 @@ CASES = [
     ("g666_eq_b25_c3", (6, 6, 6), "eq", 2.5, 3, 8, 16),
     ("g666_m52_b4_c1", (6, 6, 6), "matern52", 4.0, 1, 10, 17),
     ("g777_eq_b4_c2", (7, 7, 7), "eq", 4.0, 2, 6, 18),
+    # config C4's own parameters (bench.py c4_line, main_architecture_2_sampledistribution.py:973):
+    # EQ, beta 4, window cutoff 3, noise 1e-2 + 1e-6, ls 2h; k = 24 so the bounded-lazy form
+    # refines over several batches (about 20 CPU-minutes of reference arithmetic; --jobs 8)
+    ("g888_eq_b4_c3", (8, 8, 8), "eq", 4.0, 3, 24, 19),
 ]
 
 
@@ -77,56 +81,95 @@ def window(y, shape, cutoff):
                 yield s0 * j0 + s1 * j1 + j2
 
 
-def alg3_reference_arithmetic(alg2, cov, k, shape, cutoff):
+_W = {}  # worker state: the reference module and the jittered matrix (inherited through fork)
+
+
+def _delta(args):
+    y, A, Abar = args
+    alg2, S = _W["alg2"], _W["S"]
+    # tf.sets keep their values sorted: A \ {y} and Abar \ {y} in ascending order
+    Ay = sorted(set(A) - {y})
+    nom = float(np.asarray(alg2.nominator(y, Ay, S)).reshape(-1)[0]) - EPS
+    den = float(np.asarray(alg2.denominator(y, sorted(set(Abar) - {y}), S)).reshape(-1)[0]) - EPS
+    return 0.0 if (abs(den) < SMALL or abs(nom) < SMALL) else nom / den
+
+
+def _worker_init():
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)
+
+
+def alg3_reference_arithmetic(alg2, cov, k, shape, cutoff, jobs=1):
+    """The window loop of snippets_a3.py over the reference's own per-delta arithmetic.  The deltas
+    of one round are independent evaluations, so with ``jobs`` > 1 they run in forked worker
+    processes (one BLAS thread each): the same calls on the same inputs."""
     N = cov.shape[0]
-    S = cov + EPS * np.eye(N)
+    _W["alg2"], _W["S"] = alg2, cov + EPS * np.eye(N)
     V = list(range(N))
     A, Abar = [], list(range(N))
+    pool = None
+    if jobs > 1:
+        import multiprocessing as mp
+        pool = mp.get_context("fork").Pool(jobs, initializer=_worker_init)
 
-    def delta(y):
-        # tf.sets keep their values sorted: A \ {y} and Abar \ {y} in ascending order
-        Ay = sorted(set(A) - {y})
-        nom = float(np.asarray(alg2.nominator(y, Ay, S)).reshape(-1)[0]) - EPS
-        den = float(np.asarray(alg2.denominator(y, sorted(set(Abar) - {y}), S)).reshape(-1)[0]) - EPS
-        return 0.0 if (abs(den) < SMALL or abs(nom) < SMALL) else nom / den
+    def deltas(ys):
+        work = [(y, list(A), list(Abar)) for y in ys]
+        return pool.map(_delta, work, chunksize=1) if pool else [_delta(w) for w in work]
 
     cache = np.full(N, 1e8)
     dci = np.zeros((N, k))
-    for y in range(N):
-        cache[y] = delta(y)
+    cache[:] = deltas(range(N))
     dci[:, 0] = cache
     for i in range(k - 1):
         y = int(alg2.argmax_cache_linear(cache, A, V))
         A.append(y)
         Abar.remove(y)
         cache[y] = 0.0
-        for yj in window(y, shape, cutoff):
-            cache[yj] = 0.0 if yj in A else delta(yj)
+        win = list(window(y, shape, cutoff))
+        todo = [yj for yj in win if yj not in A]
+        vals = dict(zip(todo, deltas(todo)))
+        for yj in win:
+            cache[yj] = 0.0 if yj in A else vals[yj]
         cache[y] = 0.0
         dci[:, i + 1] = cache
+        print(f"  round {i + 1}: pick {y}", flush=True)
     A.append(int(alg2.argmax_cache_linear(cache, A, V)))
+    if pool:
+        pool.close()
+        pool.join()
     return A, cache, dci
 
 
-def main():
+def main(only=(), jobs=1):
+    """``only``: case names to (re)generate; the others keep their committed entries."""
     alg2 = _import_reference()
     alg2.print = lambda *a, **kw: None
+    path = os.path.join(HERE, "alg3_golden.json")
     golden = {}
+    if only and os.path.exists(path):
+        with open(path) as f:
+            golden = json.load(f)
     for name, shape, kind, beta, cutoff, k, seed in CASES:
+        if only and name not in only:
+            continue
         t0 = time.time()
         X = grid_points(shape, jitter=0.05, seed=seed)
         ls = 2.0 * grid_spacing(shape)
         cov = lpo.tapered_cov(X, shape, beta, kind=kind, ls=ls, diag_shift=SHIFT)
-        order, cache, dci = alg3_reference_arithmetic(alg2, cov, k, list(shape), cutoff)
+        order, cache, dci = alg3_reference_arithmetic(alg2, cov, k, list(shape), cutoff, jobs)
         np.savez_compressed(os.path.join(HERE, f"alg3_{name}.npz"), cov=cov, X=X,
                             order=np.asarray(order, dtype=np.int64), dci=dci, cache=cache)
         golden[name] = dict(shape=list(shape), kernel=kind, beta=beta, cutoff=cutoff, k=k,
                             seed=seed, ls=float(ls), diag_shift=SHIFT, jitter=0.05, order=order,
                             pick_deltas=[float(dci[a, i]) for i, a in enumerate(order)])
         print(name, order, f"{time.time() - t0:.1f} s", flush=True)
-    with open(os.path.join(HERE, "alg3_golden.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(golden, f, indent=1)
 
 
 if __name__ == "__main__":
-    main()
+    argv = sys.argv[1:]
+    jobs = 1
+    if argv[:1] == ["--jobs"]:
+        jobs, argv = int(argv[1]), argv[2:]
+    main(tuple(argv), jobs)

@@ -25,7 +25,10 @@ def test_fixture_cov_is_tapered_cov_of_X(name):
     np.testing.assert_array_equal(C, z["cov"])
 
 
-@pytest.mark.parametrize("name", NAMES)
+# the pinv restatement costs what the reference's arithmetic does (one SVD-pinv of Sigma_AbarAbar per
+# delta: ~20 CPU-minutes for the 8^3 k = 24 case), so it runs on the grids up to 7^3; the 8^3 case
+# (config C4's own parameters) pins the precision form and the C oracle, which the others tie to it
+@pytest.mark.parametrize("name", [n for n in NAMES if np.prod(load(n)[0]["shape"]) <= 343])
 def test_pinv_restatement_matches_reference_arithmetic(name):
     m, z = load(name)
     order = []

@@ -123,3 +123,17 @@ def test_data_generation_helpers():
     assert X.shape == (50, 2) and y.shape == (50,) and (np.abs(X[:, 1]) <= 1).all()
     C = dg.create_random_cov(7, np.random.default_rng(3))
     assert np.allclose(C, C.T) and np.linalg.eigvalsh(C).min() > -1e-12
+
+
+def test_gprm_oracle_matches_reference_fixture():
+    """oracle.gp.gprm_mean_cov pinned to the REFERENCE's own numpy GP posterior
+    (plot_confidence_interval.py:38-51, executed by tests/golden/make_golden_gprm.py): 5 noiseless
+    training points, EQ with l^2 = 0.3 (amplitude 1), K + 5e-5 I, mu and s2 at 700 test points.
+    The reference forms sqdist as |a|^2 + |b|^2 - 2ab, the oracle as (a - b)^2: absolute 1e-13."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "gprm_confidence.npz"))
+    m, c = ogp.gprm_mean_cov("eq", z["Xtest"], z["Xtrain"], z["ytrain"].reshape(-1), 1.0,
+                             np.sqrt(float(z["param"])), float(z["diag_shift"]), 0.0, jitter=0.0)
+    np.testing.assert_allclose(m[0], z["mu"], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(np.diag(c[0]), z["s2"], rtol=0, atol=1e-13)
+    assert z["mu"].shape == (700,) and float(z["s2"].min()) > 0

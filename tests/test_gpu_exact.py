@@ -339,6 +339,9 @@ def test_exact_128cube_regression(method):
     ((64, 64, 64), 50, 2, "matern52", 3),
     ((48, 40, 56), 60, 4, "matern32", 5),
     ((96, 80, 72), 40, 3, "eq", 7),
+    # k > 90: nr(nr + 1) exceeds the window kernel's LDS row budget, so the factor rows take the
+    # global-memory path (stage_rows / wave_new_row) for the late rounds
+    ((48, 48, 48), 110, 3, "eq", 9),
 ])
 def test_bounded_alg3_matches_c_oracle_at_scale(shape, k, cutoff, kind, seed):
     """GPU picks bit-exact against the CPU: the bounded-lazy algorithm 3 on the device and the

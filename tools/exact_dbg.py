@@ -3,7 +3,9 @@ tools/build_exact_variant.sh dbg -DVGPOSP_EXACT_DBG=1; run with
 VGPOSP_LIB=$PWD/tools/variants/lib_dbg.so python tools/exact_dbg.py [--one-level]).
 Prints the mean phase durations (us) of the stall kernel and the step kernel over one 128^3 run:
 stall: argmax | top-B | slot staging | slot ranking | batch write;
-step: window keys | argmax | slot lookup | pick + key refresh | factor rows."""
+step: window keys | argmax | slot lookup | pick + key refresh | factor rows;
+window (workgroup 0, wave 0): pick / row staging | candidate right-hand sides | new factor row |
+barrier | substitutions."""
 import ctypes
 import json
 import os
@@ -27,13 +29,14 @@ buf = (ctypes.c_ulonglong * (64 * 8))()
 lib.vgposp_exact_dbg(buf)  # reset
 out = {}
 for kind, name, phases in ((1, "stall", ["argmax", "topb", "stage", "rank", "write"]),
-                           (2, "step", ["window_keys", "argmax", "slot", "pick_keys", "rows"])):
+                           (2, "step", ["window_keys", "argmax", "slot", "pick_keys", "rows"]),
+                           (3, "window", ["stage", "rhs", "new_row", "sync", "subst"])):
     out[name] = {"phases": phases}
 run.run()
 torch.cuda.synchronize()
 lib.vgposp_exact_dbg(buf)
 rec = np.frombuffer(buf, dtype=np.uint64).reshape(64, 8).astype(np.int64)
-for kind, name in ((1, "stall"), (2, "step")):
+for kind, name in ((1, "stall"), (2, "step"), (3, "window")):
     r = rec[rec[:, 7] == kind]
     if len(r) == 0:
         continue

@@ -1382,3 +1382,179 @@ extern "C" int vgposp_gemm(int transa, int transb, int64_t m, int64_t n, int64_t
   return gemm_launch(transa, transb, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, uplo_c, tri_a,
                      tri_b, as_stream(stream));
 }
+
+
+// ---------------------------------------------------------------------------------------------
+// Round 5 hygiene: the explicitly sequenced K-loop (formerly -DVGPOSP_GEMM_ASM=1/2 and
+// -DVGPOSP_GEMM_ACC_AGPR=1 inside vgposp_amd/csrc/gemm.hip's gemm_glds_body).  Measured slower
+// than the compiler-scheduled loop (profiles/r3_gemm_asm_ab.txt); NOT BUILT.  The helpers, then
+// the loop as it sat in the kernel body in front of the default loop:
+// ---- explicitly sequenced K-loop (VGPOSP_GEMM_ASM) -------------------------------------------
+// Every LDS fragment read, LDS-DMA piece, MFMA, counter wait and barrier of the main loop is its
+// own `asm volatile` statement, so the issue order is the one written below (volatile asm is never
+// reordered against volatile asm); the compiler only places the address arithmetic between them.
+// The fragments of k-slice s + 1 are read while slice s is multiplied (two fragment sets), so a
+// wave never waits on LDS latency inside a K-tile.  The compiler's waitcnt pass does not see into
+// inline asm: every wait is explicit, and a wait takes the fragments it guards as in/out operands
+// so that no use (mask, MFMA) can be scheduled above it.
+#ifndef VGPOSP_GEMM_ASM
+#define VGPOSP_GEMM_ASM 0
+#endif
+
+template <int OFF>
+__device__ __forceinline__ double ds_rd(uint32_t addr) {
+  double v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+
+__device__ __forceinline__ void lgkm_wait0(double (&a)[4], double (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]),
+                 "+v"(b[3]));
+}
+
+#ifndef VGPOSP_GEMM_ACC_AGPR
+#define VGPOSP_GEMM_ACC_AGPR 0
+#endif
+// VGPOSP_GEMM_ACC_AGPR: accumulators (srcC / vdst) in AGPRs, so the MFMA's 8-register srcC read
+// and result write do not share the architectural VGPR file with the fragment loads
+__device__ __forceinline__ void mfma_asm(dbl4& c, double a, double b) {
+#if VGPOSP_GEMM_ACC_AGPR
+  asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+#else
+  asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+#endif
+}
+
+// One LDS-DMA piece: 64 lanes x 16 bytes from src (per lane) to LDS [lds, lds + 1 KiB).
+__device__ __forceinline__ void dma_asm(const double* src, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(lds)
+               : "memory", "m0");
+}
+
+template <bool KC>
+__device__ __forceinline__ const double* glds_src(const double* base, int64_t ld, int64_t r0,
+                                                  int64_t k0, int64_t R, int64_t K, int i, int lane) {
+  if (KC) {
+    const int row = 8 * i + (lane >> 3);
+    const int kp = (lane & 7) ^ ((row & 15) >> 1);
+    const int64_t gr = min(r0 + row, R - 1);
+    const int64_t gk = min(k0 + 2 * kp, K - 2);
+    return base + gr * ld + gk;
+  }
+  const int p = lane ^ ((i & 1) << 3);
+  const int64_t gk = min(k0 + i, K - 1);
+  const int64_t gc = min(r0 + 2 * p, R - 2);
+  return base + gk * ld + gc;
+}
+
+// Fragments 0..3 of one operand for one k-slice: fragment 2q + p at base[p] + q * D bytes
+// (D = 4096 for a k-contiguous image, 256 for a row-contiguous one).
+template <bool KC>
+__device__ __forceinline__ void rd_frags(uint32_t b0, uint32_t b1, double (&f)[4]) {
+  constexpr int D = KC ? 4096 : 256;
+  f[0] = ds_rd<0>(b0);
+  f[1] = ds_rd<0>(b1);
+  f[2] = ds_rd<D>(b0);
+  f[3] = ds_rd<D>(b1);
+}
+
+
+#if VGPOSP_GEMM_ASM
+  static_assert(NST == 2 && NSUB == 1 && FI == 4 && PPW == 8, "sequenced loop: 2-stage 128x128");
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  // per-lane byte offsets (within a stage) of fragments 0 and 1 of each k-slice
+  uint32_t ab[4][2], bb[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      ab[ks][q] = 8 * frag_off<A_KC>((wm * WROWS) % GBM + q * 16 + fr, ks * 4 + fk);
+      bb[ks][q] = 8 * (NSUB * OPND_ELEMS + frag_off<B_KC>(wn * 64 + q * 16 + fr, ks * 4 + fk));
+    }
+  // ASM = 1: each K-tile starts with the counted wait + barrier.  ASM = 2: the barrier sits
+  // before the tile's LAST k-slice, whose fragments are already in registers, and the next tile's
+  // slice-0 reads and the tile-after-next's DMA pieces are issued behind it, so the barrier skew
+  // and the LDS latency of the tile change hide under that slice's 16 MFMAs.
+  constexpr bool XT = VGPOSP_GEMM_ASM >= 2;
+  auto dma_piece = [&](int tt, int q) {  // piece q (0..7) of this wave for K-tile tt
+    const int op = q / PO, jj = wave * PO + q % PO;
+    const int64_t kk = kbeg + (int64_t)tt * GBK;
+    const double* src = op == 0 ? glds_src<A_KC>(gA, p.lda, m0, kk, p.m, p.k, jj, lane)
+                                : glds_src<B_KC>(gB, p.ldb, n0, kk, p.n, p.k, jj, lane);
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (int)(lds0 + (uint32_t)(((tt & 1) * SE + op * OPND_ELEMS + jj * 128) * 8)));
+    dma_asm(src, dst);
+  };
+  double fa[2][4], fb[2][4];
+  if (XT && T > 0) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    rd_frags<A_KC>(lds0 + ab[0][0], lds0 + ab[0][1], fa[0]);
+    rd_frags<B_KC>(lds0 + bb[0][0], lds0 + bb[0][1], fb[0]);
+    if (T > 1) {
+#pragma unroll
+      for (int q = 0; q < PPW; ++q) dma_piece(1, q);
+    }
+  }
+  for (int t = 0; t < T; ++t) {
+    const uint32_t sb = lds0 + (uint32_t)((t & 1) * SE * 8);
+    const uint32_t nb = lds0 + (uint32_t)(((t + 1) & 1) * SE * 8);
+    const bool more = t + 1 < T;
+    const int64_t k0 = kbeg + (int64_t)t * GBK;
+    const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + TBM && k0 + GBK > m0) ||
+                      (TRIB && k0 < n0 + GBN && k0 + GBK > n0);
+    if (!XT) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      rd_frags<A_KC>(sb + ab[0][0], sb + ab[0][1], fa[0]);
+      rd_frags<B_KC>(sb + bb[0][0], sb + bb[0][1], fb[0]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = ks & 1;
+      lgkm_wait0(fa[c], fb[c]);
+      if (mask) {
+        const int64_t gk = k0 + ks * 4 + fk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t gm = m0 + wm * WROWS + i * 16 + fr;
+          if (gk >= kend || (TRIA && (TA ? gm > gk : gk > gm))) fa[c][i] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t gn = n0 + wn * 64 + j * 16 + fr;
+          if (gk >= kend || (TRIB && (TB ? gk > gn : gn > gk))) fb[c][j] = 0.0;
+        }
+      }
+      if (ks < 3) {
+        rd_frags<A_KC>(sb + ab[ks + 1][0], sb + ab[ks + 1][1], fa[c ^ 1]);
+        rd_frags<B_KC>(sb + bb[ks + 1][0], sb + bb[ks + 1][1], fb[c ^ 1]);
+      } else if (XT && more) {
+        // every wave has its tile-t fragments in registers and its tile-(t+1) pieces landed
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        rd_frags<A_KC>(nb + ab[0][0], nb + ab[0][1], fa[0]);
+        rd_frags<B_KC>(nb + bb[0][0], nb + bb[0][1], fb[0]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          mfma_asm(acc[i][j], fa[c][i], fb[c][j]);
+          if (!XT) {
+            // the next K-tile's 8 pieces of this wave: one per 4 MFMAs of slices 0 and 1
+            if (ks < 2 && j == 0 && more) dma_piece(t + 1, ks * 4 + i);
+          } else {
+            // the tile-after-next's pieces into the buffer tile t just released: one per 2 MFMAs
+            // of the last slice
+            if (ks == 3 && (j & 1) == 0 && t + 2 < T) dma_piece(t + 2, i * 2 + (j >> 1));
+          }
+        }
+    }
+  }
+  // f64 MFMA results are read by VALU below: cover the XDL write -> VALU read hazard, which the
+  // compiler's hazard recognizer cannot see through inline asm
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  if (false)
+#endif

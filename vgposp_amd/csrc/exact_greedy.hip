@@ -45,10 +45,7 @@ constexpr int EB = 256;      // cache entries per block key
 constexpr int ESB = 64;      // blocks per superblock key
 constexpr int CG_BLOCKS = 1024;
 constexpr int CG_T = 256;
-#ifndef VGPOSP_CG_SEG  // (A/B: lanes per diamond row of the 7-point CG walk; 64 = one row per wave)
-#define VGPOSP_CG_SEG 16
-#endif
-constexpr int CG_SEG = VGPOSP_CG_SEG;
+constexpr int CG_SEG = 16;  // lanes per diamond row of the 7-point CG walk (64: one row per wave, slower)
 constexpr int CG_RPW = 64 / CG_SEG;  // diamond rows per wave
 constexpr int SEL_THREADS = 1024;
 
@@ -326,9 +323,6 @@ __global__ __launch_bounds__(64) void exact_gersh_final_kernel(double* part, int
 // node + off_o or -1); lane l holds nodes l, l + 64, ... in registers, p is exchanged through a
 // wave-private LDS vector.  Step it touches only the tab_cnt[it + 1] nodes A p_it can reach.
 // qhi[y] = hi_scale * sum_i alpha_i |r_i|^2, hi_scale = (1 + margin) / (1 - 4 rho^(2K)).
-#ifndef VGPOSP_BND_RR
-#define VGPOSP_BND_RR 0
-#endif
 // Upper bounds of Q_yy = e_y^T (S + eps I)^-1 e_y from K CG steps on (S + eps I) x = e_y, x0 = 0.
 // The CG estimate g_K = sum_k gamma_k |r_k|^2 (gamma_k = alpha_k) is the Gauss-quadrature LOWER
 // bound, and Q_yy - g_K = |x - x_K|_A^2.  Two upper bounds:
@@ -351,9 +345,7 @@ __device__ __forceinline__ double bound_value(double g, double gmu, double rrK, 
   return mu > 0.0 ? hi_scale * fma(gmu, rrK, g) : hi_scale * g;
 }
 
-#ifndef VGPOSP_BND_GRID  // (A/B: workgroups of the all-candidate bounds launch, at most)
-#define VGPOSP_BND_GRID 65536
-#endif
+constexpr int BND_GRID = 65536;  // workgroups of an all-candidate bounds launch, at most
 constexpr int BND_T = 256;
 constexpr int BND_WAVES = BND_T / 64;
 constexpr int BND_SMAX = 14;
@@ -379,15 +371,10 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
   // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs, so XCD x (= blockIdx.x
   // mod 8) walks its own contiguous eighth of the candidates and neighbouring candidates, whose
   // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
-#if VGPOSP_BND_RR  // (A/B: the plain round-robin order)
-  for (long long y = c0 + (long long)blockIdx.x * BND_WAVES + wave; y < c1;
-       y += (long long)gridDim.x * BND_WAVES) {
-#else
   const long long per_xcd = (c1 - c0 + 7) / 8, xlo = c0 + (blockIdx.x & 7) * per_xcd;
   const long long xhi = min(c1, xlo + per_xcd);
   for (long long y = xlo + (long long)(blockIdx.x >> 3) * BND_WAVES + wave; y < xhi;
        y += (long long)(gridDim.x >> 3) * BND_WAVES) {
-#endif
     const long long y0 = y / (I1 * I2), y1 = (y / I2) % I1, y2 = y % I2;
     int gi[BND_SMAX];  // grid index (n < 2^31, checked by the caller) or -1
     double r[BND_SMAX], p[BND_SMAX], q[BND_SMAX];
@@ -463,14 +450,6 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_kernel(
 // coefficients (SM x (M1 + 1) doubles per lane) are loaded into registers once, all loads in
 // flight together, so its K steps run on registers and LDS only (the generic kernel above waits on
 // one coefficient load at a time).  Neighbours outside the table read a zero LDS entry.
-#ifndef VGPOSP_BND_WPE  // (A/B: waves per SIMD the register allocation must allow; 0 = default)
-#define VGPOSP_BND_WPE 0
-#endif
-#if VGPOSP_BND_WPE
-#define VG_BND_ATTR __attribute__((amdgpu_waves_per_eu(VGPOSP_BND_WPE)))
-#else
-#define VG_BND_ATTR
-#endif
 // A coefficient row (M doubles of the 16-byte-aligned padded row gi, zeros for gi < 0) in
 // two-double loads.
 template <int M>
@@ -557,7 +536,7 @@ __device__ __forceinline__ double bounds_cg(const double (&c)[SM][M1 + 1],
 }
 
 template <int SM, int M1, bool LIST = false>
-__global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
+__global__ __launch_bounds__(BND_T) void exact_bounds_reg_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
     const int* __restrict__ tab_cnt, int T, int K, double hi_scale, double mu, long long c0,
@@ -612,12 +591,6 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
   // reach tables share most coefficient rows, meet in the same L2 (gridDim.x is a multiple of 8)
   // LIST: the candidates list[0 .. *list_count) (the tightening of a refinement event)
   const long long nlist = LIST ? (long long)*list_count : 0;
-#if VGPOSP_BND_RR  // (A/B: the plain round-robin order)
-  for (long long it_y = LIST ? (long long)blockIdx.x * BND_WAVES + wave
-                             : c0 + (long long)blockIdx.x * BND_WAVES + wave;
-       LIST ? it_y < nlist : it_y < c1; it_y += (long long)gridDim.x * BND_WAVES) {
-    const long long y = LIST ? list[it_y] : it_y;
-#else
   const long long per_xcd = (c1 - c0 + 7) / 8, xlo = c0 + (blockIdx.x & 7) * per_xcd;
   const long long xhi = min(c1, xlo + per_xcd);
   for (long long it_y = LIST ? (long long)blockIdx.x * BND_WAVES + wave
@@ -625,7 +598,6 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
        LIST ? it_y < nlist : it_y < xhi;
        it_y += LIST ? (long long)gridDim.x * BND_WAVES : (long long)(gridDim.x >> 3) * BND_WAVES) {
     const long long y = LIST ? list[it_y] : it_y;
-#endif
     const unsigned yu = (unsigned)y;
     const int y0 = (int)(yu / I12), yr = (int)(yu - (unsigned)y0 * I12);
     const int y1 = yr / I2i, y2 = yr - y1 * I2i;
@@ -648,99 +620,177 @@ __global__ __launch_bounds__(BND_T) VG_BND_ATTR void exact_bounds_reg_kernel(
   }
 }
 
-// The all-candidate bounds for K <= BT_H steps on the 7-point stencil (one reach-table slot per
-// lane, T <= 64), tiled: a workgroup takes a BT_E^3 tile of candidates and stages the coefficient
-// rows of the tile and its BT_H halo (BT_B^3 = 1,000 rows, 56 KB as seven planes) into LDS once,
-// with neighbouring rows on neighbouring lanes; a candidate's 63 rows are then LDS reads, not 63
-// scattered 64-byte global loads (15.6 staged rows per candidate against 63 loaded ones).  The CG
-// is exactly exact_bounds_reg_kernel's (bounds_cg, the same coefficients in the same order), so
-// the bounds are bit-identical.  A table offset outside the halo (a stencil with longer reach)
-// reads its row from global memory, as the register kernel does.
-// A/B only (-DVGPOSP_BND_TILE=1, profiles/r4_c4_bounds_tile.jsonl): bounds bit-identical, but the
-// 128^3 K = 3 pass takes 1.81 ms against the register kernel's 1.70.  The coefficient loads were
-// not the bound: a candidate is ~500 wave instructions of CG (the six gathers, FMAs, two wave
-// sums and three fp64 divisions per step), and the 61 KB of LDS halves the waves per SIMD.
-constexpr int BT_E = 4, BT_H = 3, BT_B = BT_E + 2 * BT_H, BT_ROWS = BT_B * BT_B * BT_B;
-constexpr int BT_T = 512, BT_WAVES = BT_T / 64;
+// Sum over the aligned groups of LPC lanes (LPC = 2, 4, 8, 16, 32 or 64), every lane of a group
+// returning its group's sum.  Intra-row DPP for the small groups — quad_perm for xor 1 / 2, then
+// row_half_mirror (lane i -> 7 - i within 8: the other quad's sum once each quad is uniform) and
+// row_mirror (i -> 15 - i within 16: the other half-row's) — and the CDNA4 permlane swaps above
+// 16.  Every step adds two group-uniform partial sums with a commutative +, so the lanes of a
+// group end with bit-identical values.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const unsigned hi =
+      (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
 
-template <int M1>
-__global__ __launch_bounds__(BT_T) void exact_bounds_tile_kernel(
+template <int LPC>
+__device__ __forceinline__ double group_sum(double v) {
+  static_assert(LPC == 2 || LPC == 4 || LPC == 8 || LPC == 16 || LPC == 32 || LPC == 64,
+                "group of 2..64 lanes");
+  v += dpp64<0xB1>(v);  // quad_perm [1,0,3,2]
+  if constexpr (LPC >= 4) v += dpp64<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (LPC >= 8) v += dpp64<0x141>(v);  // row_half_mirror
+  if constexpr (LPC >= 16) v += dpp64<0x140>(v); // row_mirror
+  if constexpr (LPC >= 32) v = wave_step<16>(v, [](double a, double b) { return a + b; });
+  if constexpr (LPC >= 64) v = wave_step<32>(v, [](double a, double b) { return a + b; });
+  return v;
+}
+
+// bounds_cg with G candidates per wave: candidate g of the wave on lanes [g LPC, (g + 1) LPC),
+// reach-table node j = s LPC + l on slot s of group lane l (T <= 64 nodes, so G slots per lane).
+// The wave-uniform part of a CG step (the two reductions, three divisions, the Radau update) is
+// then ONE instruction stream for G candidates instead of one per candidate, and the reductions
+// are log2(LPC) intra-row steps.  pl: the group's 64 + 1 LDS doubles (the last one 0: the
+// neighbour of a node outside the table).
+template <int G>
+__device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const unsigned (&nbo)[G][3],
+                                                double* pl, const int* cntl, int K, double hi_scale,
+                                                double mu, int l) {
+  constexpr int LPC = 64 / G;
+  const char* plb = reinterpret_cast<const char*>(pl);
+  double r[G], p[G], q[G];
+#pragma unroll
+  for (int s = 0; s < G; ++s) {
+    r[s] = (s == 0 && l == 0) ? 1.0 : 0.0;
+    p[s] = r[s];
+    pl[s * LPC + l] = r[s];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double rr = 1.0, g = 0.0, gmu = mu > 0.0 ? 1.0 / mu : 0.0;
+  for (int it = 0; it < K; ++it) {
+    const int cnt = cntl[it + 1];
+    double pq = 0.0;
+#pragma unroll
+    for (int s = 0; s < G; ++s) {
+      q[s] = 0.0;
+      if (s * LPC < cnt) {
+        double acc = c[s][0] * p[s];
+#pragma unroll
+        for (int o = 0; o < 6; ++o) {
+          const unsigned off = (nbo[s][o >> 1] >> (16 * (o & 1))) & 0xffffu;
+          acc = fma(c[s][1 + o], *reinterpret_cast<const double*>(plb + off), acc);
+        }
+        q[s] = s * LPC + l < cnt ? acc : 0.0;
+        pq = fma(p[s], q[s], pq);
+      }
+    }
+    pq = group_sum<LPC>(pq);
+    const double alpha = rr / pq;
+    g = fma(alpha, rr, g);
+    if (it + 1 == K && mu <= 0.0) break;
+    double rn = 0.0;
+#pragma unroll
+    for (int s = 0; s < G; ++s) {
+      r[s] = fma(-alpha, q[s], r[s]);
+      rn = fma(r[s], r[s], rn);
+    }
+    rn = group_sum<LPC>(rn);
+    const double beta = rn / rr;  // = delta_{k+1}
+    if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, beta);
+    rr = rn;
+    if (it + 1 == K) break;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s = 0; s < G; ++s) {
+      p[s] = fma(beta, p[s], r[s]);
+      if (s * LPC < cnt) pl[s * LPC + l] = p[s];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  return bound_value(g, gmu, rr, mu, hi_scale);
+}
+
+// The all-candidate bounds of exact_bounds_reg_kernel<1, 6> (7-point stencil, reach table of
+// T <= 64 nodes: K <= 3) with G candidates per wave (bounds_cg_grp): G consecutive candidates
+// y .. y + G - 1 share most of their coefficient rows, so their loads meet in L1 / L2.
+#ifndef VGPOSP_BND_G
+#define VGPOSP_BND_G 8
+#endif
+template <int G>
+__global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
     const int* __restrict__ tab_cnt, int T, int K, double hi_scale, double mu, long long c0,
-    long long c1, double* __restrict__ qhi, int tile_lo, int tile_hi, int per_xcd) {
-  constexpr int M = M1 + 1;
-  __shared__ double cl[M][BT_ROWS];
-  __shared__ double plds[BT_WAVES][64 + 1];
+    long long c1, double* __restrict__ qhi) {
+  constexpr int LPC = 64 / G, M1 = 6, M = 7;
+  __shared__ double plds[BND_WAVES][G][65];
   __shared__ short nbl[64 * M1];
+  __shared__ short offl[3 * 64];
   __shared__ int cntl[4 * BND_SMAX + 1];
-  // XCD-aware: XCD x (= blockIdx.x mod 8) takes its own contiguous run of tiles, so the halos
-  // neighbouring tiles share meet in the same L2
-  const int tile = tile_lo + (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
-  if (tile >= tile_hi) return;  // (whole workgroup)
-  const int I0i = (int)I0, I1i = (int)I1, I2i = (int)I2;
-  const int TD1 = (I1i + BT_E - 1) / BT_E, TD2 = (I2i + BT_E - 1) / BT_E;
-  const int t0 = tile / (TD1 * TD2) * BT_E, t1 = tile / TD2 % TD1 * BT_E, t2 = tile % TD2 * BT_E;
-  for (int i = threadIdx.x; i < 64 * M1; i += BT_T) {
+  for (int i = threadIdx.x; i < 64 * M1; i += BND_T) {
     const int v = i < T * M1 ? tab_nb[i] : -1;
     nbl[i] = (short)(v >= 0 ? v : 64);
   }
-  for (int i = threadIdx.x; i <= K; i += BT_T) cntl[i] = tab_cnt[i];
-  for (int b = threadIdx.x; b < BT_ROWS; b += BT_T) {
-    const int g0 = t0 - BT_H + b / (BT_B * BT_B), g1 = t1 - BT_H + b / BT_B % BT_B,
-              g2 = t2 - BT_H + b % BT_B;
-    int gi = -1;
-    if ((unsigned)g0 < (unsigned)I0i && (unsigned)g1 < (unsigned)I1i && (unsigned)g2 < (unsigned)I2i)
-      gi = (g0 * I1i + g1) * I2i + g2;
-    double row[M];
-    load_coef_row<M>(coef, gi, row);
-#pragma unroll
-    for (int o = 0; o < M; ++o) cl[o][b] = row[o];
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double* pl = plds[wave];
-  if (lane == 0) pl[64] = 0.0;
+  for (int i = threadIdx.x; i < 3 * 64; i += BND_T) offl[i] = (short)(i < 3 * T ? tab_off[i] : 0);
+  for (int i = threadIdx.x; i <= K; i += BND_T) cntl[i] = tab_cnt[i];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gl = lane / LPC, l = lane % LPC;
+  double* pl = plds[wave][gl];
+  if (l == 0) pl[64] = 0.0;
   __syncthreads();
-  constexpr int NP = (M1 + 1) / 2;
-  unsigned nbo[1][NP];
+  // node j = s LPC + l: its neighbours' byte offsets into pl, two per register, and its table
+  // offset as three signed bytes (-1: beyond the table)
+  unsigned nbo[G][3];
+  int ofr[G];
 #pragma unroll
-  for (int o = 0; o < NP; ++o) {
-    const unsigned lo = 8u * (unsigned)nbl[lane * M1 + 2 * o];
-    const unsigned hi = 2 * o + 1 < M1 ? 8u * (unsigned)nbl[lane * M1 + 2 * o + 1] : 0u;
-    nbo[0][o] = lo | (hi << 16);
+  for (int s = 0; s < G; ++s) {
+    const int j = s * LPC + l;
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+      nbo[s][o] = (8u * (unsigned)nbl[j * M1 + 2 * o]) | ((8u * (unsigned)nbl[j * M1 + 2 * o + 1]) << 16);
+    ofr[s] = j < T ? ((offl[3 * j] + 128) | ((offl[3 * j + 1] + 128) << 8) |
+                      ((offl[3 * j + 2] + 128) << 16))
+                   : -1;
   }
-  // the lane's node: its offset in the staged box (inbox) or, outside the halo, its grid offset
-  int o0 = 0, o1 = 0, o2 = 0;
-  const bool valid = lane < T;
-  if (valid) o0 = tab_off[3 * lane], o1 = tab_off[3 * lane + 1], o2 = tab_off[3 * lane + 2];
-  const bool inbox = valid && abs(o0) <= BT_H && abs(o1) <= BT_H && abs(o2) <= BT_H;
-  const int dob = (o0 * BT_B + o1) * BT_B + o2;
-  for (int lc = wave; lc < BT_E * BT_E * BT_E; lc += BT_WAVES) {
-    const int l0 = lc / (BT_E * BT_E), l1 = lc / BT_E % BT_E, l2 = lc % BT_E;
-    const int y0 = t0 + l0, y1 = t1 + l1, y2 = t2 + l2;
-    if (y0 >= I0i || y1 >= I1i || y2 >= I2i) continue;  // (whole wave)
-    const long long y = ((long long)y0 * I1i + y1) * I2i + y2;
-    if (y < c0 || y >= c1) continue;
-    double c[1][M];
-    if (inbox) {
-      const int b = ((l0 + BT_H) * BT_B + (l1 + BT_H)) * BT_B + (l2 + BT_H) + dob;
+  const int I0i = (int)I0, I1i = (int)I1, I2i = (int)I2;
+  const unsigned I12 = (unsigned)(I1i * I2i);
+  // XCD-aware order as exact_bounds_reg_kernel: XCD x (= blockIdx.x mod 8) walks its own
+  // contiguous eighth of [c0, c1), G candidates per wave
+  const long long per_xcd = (c1 - c0 + 7) / 8, xlo = c0 + (blockIdx.x & 7) * per_xcd;
+  const long long xhi = min(c1, xlo + per_xcd);
+  for (long long yb = xlo + ((long long)(blockIdx.x >> 3) * BND_WAVES + wave) * G; yb < xhi;
+       yb += (long long)(gridDim.x >> 3) * BND_WAVES * G) {
+    const long long y = yb + gl;
+    const bool live = y < xhi;
+    const unsigned yu = (unsigned)(live ? y : yb);
+    const int y0 = (int)(yu / I12), yr = (int)(yu - (unsigned)y0 * I12);
+    const int y1 = yr / I2i, y2 = yr - y1 * I2i;
+    double c[G][M];
 #pragma unroll
-      for (int o = 0; o < M; ++o) c[0][o] = cl[o][b];
-    } else {
+    for (int s = 0; s < G; ++s) {
       int gi = -1;
-      const int g0 = y0 + o0, g1 = y1 + o1, g2 = y2 + o2;
-      if (valid && (unsigned)g0 < (unsigned)I0i && (unsigned)g1 < (unsigned)I1i &&
-          (unsigned)g2 < (unsigned)I2i)
-        gi = (g0 * I1i + g1) * I2i + g2;
-      load_coef_row<M>(coef, gi, c[0]);
+      if (ofr[s] >= 0) {
+        const int g0 = y0 + (ofr[s] & 255) - 128, g1 = y1 + ((ofr[s] >> 8) & 255) - 128,
+                  g2 = y2 + ((ofr[s] >> 16) & 255) - 128;
+        if ((unsigned)g0 < (unsigned)I0i && (unsigned)g1 < (unsigned)I1i &&
+            (unsigned)g2 < (unsigned)I2i)
+          gi = (g0 * I1i + g1) * I2i + g2;
+      }
+      load_coef_row<M>(coef, gi, c[s]);
     }
-    const double ub = bounds_cg<1, M1>(c, nbo, pl, cntl, K, hi_scale, mu, lane);
-    if (lane == 0) qhi[y] = ub;
+    const double ub = bounds_cg_grp<G>(c, nbo, pl, cntl, K, hi_scale, mu, l);
+    if (live && l == 0) qhi[y] = ub;
   }
 }
 
-// Round 0 (snippets_a3.py:77-124): A empty, nom = s_yy, denom = 1 / Q_yy - eps (an upper bound of
-// the delta where qexact[y] = 0).
 template <int KIND>
 __global__ __launch_bounds__(256) void exact_score_kernel(EArgs a, const double* __restrict__ qdiag,
                                                           const unsigned char* __restrict__ qexact,
@@ -985,7 +1035,7 @@ __device__ long long block_argmax(const ExactWS& w, long long nsb) {
   double v = 0.0;
   long long idx = -1;
   for (long long s = t; s < nsb; s += SEL_THREADS) {
-    if (key_gt(w.sval[s], w.sidx[s], v, idx)) {
+    if (w.sidx[s] >= 0 && key_gt(w.sval[s], w.sidx[s], v, idx)) {
       v = w.sval[s];
       idx = w.sidx[s];
     }
@@ -1875,6 +1925,8 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
                                                            const long long* picks) {
   __shared__ double sm[ROWS_LDS];
   __shared__ StagedPicks sp;
+  DBG_DECL
+  DBG_T(0)
   const long long at = picks[round];
   if (at < 0) return;
   const Window v = window_of(a, at);
@@ -1889,6 +1941,7 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
                            : (__syncthreads(), global_rows(w, a.kmax));
   // the candidate's right-hand sides need only the staged picks: loaded before the new row (whose
   // chain they then overlap), the substitutions after it
+  DBG_T(1)
   const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool live = e < v.w0 * v.w1 * v.w2;
   const long long y = live ? ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) *
@@ -1903,8 +1956,11 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
     qyy = qdiag[y];
     ex = w.qexact[y] == 1;
   }
+  DBG_T(2)
   if ((threadIdx.x >> 6) < 2) wave_new_row<KIND>(a, w, round, L, sp, lds ? sm : nullptr);
+  DBG_T(3)
   __syncthreads();
+  DBG_T(4)
   if (!live) return;
   if (picked) {
     if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
@@ -1914,6 +1970,10 @@ __global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
+  }
+  DBG_T(5)
+  if (blockIdx.x == 0) {
+    DBG_END(3)
   }
 }
 
@@ -2498,24 +2558,9 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   const long long waves = c1 - c0;
   const unsigned blocks =
       (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES), 8LL),
-                                         VGPOSP_BND_GRID / 8));
+                                         BND_GRID / 8));
   double* out = const_cast<double*>(qdiag);
   const long long lc0 = c0, lc1 = c1;
-#ifndef VGPOSP_BND_TILE  // (A/B: 1 = the tiled kernel for T <= 64; measured slower, see there)
-#define VGPOSP_BND_TILE 0
-#endif
-  if (VGPOSP_BND_TILE && a.m1 == 6 && T <= 64) {
-    // the tiles of the grid planes y0 that [c0, c1) touches
-    const long long plane = a.I1 * a.I2;
-    const long long TD1 = ceil_div(a.I1, (long long)BT_E), TD2 = ceil_div(a.I2, (long long)BT_E);
-    const long long lo = c0 / plane / BT_E * TD1 * TD2, hi = ((c1 - 1) / plane / BT_E + 1) * TD1 * TD2;
-    const long long per_xcd = ceil_div(hi - lo, 8LL);
-    hipLaunchKernelGGL(exact_bounds_tile_kernel<6>, dim3((unsigned)(8 * per_xcd)), dim3(BT_T), 0, s,
-                       w.coef, a.I0, a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0,
-                       lc1, out, (int)lo, (int)hi, (int)per_xcd);
-    VG_LAUNCH_CHECK();
-    return 0;
-  }
 #define VG_BOUNDS_REG(SMV)                                                                     \
   if (T <= 64 * SMV) {                                                                           \
     hipLaunchKernelGGL((exact_bounds_reg_kernel<SMV, 6>), dim3(blocks), dim3(BND_T), 0, s, w.coef, \
@@ -2523,6 +2568,16 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
                        out);                                                                      \
     VG_LAUNCH_CHECK();                                                                           \
     return 0;                                                                                    \
+  }
+  if (a.m1 == 6 && T <= 64 && VGPOSP_BND_G > 1) {  // K <= 3: G candidates per wave
+    constexpr int G = VGPOSP_BND_G;
+    const unsigned gblocks =
+        (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES * G), 8LL),
+                                           BND_GRID / 8));
+    hipLaunchKernelGGL(exact_bounds_grp_kernel<G>, dim3(gblocks), dim3(BND_T), 0, s, w.coef, a.I0,
+                       a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0, lc1, out);
+    VG_LAUNCH_CHECK();
+    return 0;
   }
   if (a.m1 == 6) {  // the 7-point taper support of the reference's beta = 4
     VG_BOUNDS_REG(1)

@@ -263,7 +263,9 @@ __device__ __forceinline__ void reduce_keys(const double* val, const long long* 
   v = -DBL_MAX;
   i = -1;
   for (int64_t e = threadIdx.x; e < nf; e += blockDim.x) {
-    if (key_gt(val[e], idx[e], v, i)) {
+    // idx < 0: a chunk with no candidate left (wave_keymax returns (0.0, -1) for it); it must not
+    // enter the comparison, or its 0.0 would shut out a real candidate with a value <= 0
+    if (idx[e] >= 0 && key_gt(val[e], idx[e], v, i)) {
       v = val[e];
       i = idx[e];
     }

@@ -623,12 +623,22 @@ class ExactWindowGreedy:
             call("vgposp_exact_pretighten", *args, *targs[:-1], int(self.pretighten), st)
         call("vgposp_exact_steps", *args, 0, 1, k, B, pk, pd, st)  # round 0 stalls: nothing refined
         issued, reads = 1, 0
+        # every host read either issues at least one new round or clears a stall by refining /
+        # tightening at least one candidate; each candidate is refined at most once per bound
+        # level, so a correct run needs far fewer reads than this cap
+        max_reads = k * (2 + REFINE_BATCH_MAX) + 16
         while True:
             # stall round, CG batch, refined-unpicked, events, refined, age, tightening list, tightened
             c = ctl.cpu().tolist()
             reads += 1
+            if reads > max_reads:
+                raise RuntimeError(f"run_bounded: {reads} control-block reads for k = {k} "
+                                   f"(control block {c}): the device rounds are not progressing")
             stall = c[0]
             if stall >= 0:
+                if c[1] == 0 and c[6] == 0:
+                    raise RuntimeError(f"run_bounded: round {stall} stalled with neither a CG "
+                                       f"batch nor a tightening list (control block {c})")
                 if c[6] > 0:
                     if tight is None:
                         raise RuntimeError("tightening list without a K_hi table")

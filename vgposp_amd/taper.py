@@ -5,14 +5,18 @@ The reference's scaling answer is its algorithm 3 (``snippets_a3.sparse_placemen
 ``snippets_a3.py:43-364``) on the beta-decay local kernel of
 ``main_architecture_2_sampledistribution.py:355-421``: covariances are multiplied by
 ``exp(-(beta d)^2 / (2 pi))`` of the index distance d and zeroed where that decay is < 0.01
-(``BETA_val = 4`` there, with ``cutoff = 3``, ``:973``).  ``taper_support`` is the non-zero
+(``decay_fn``, ``:390-393``; ``BETA_val = 4`` there, with ``cutoff = 3``, ``:973``).  That is the
+filter the reference intends, not the one its code computes: the ``tf.cond`` at ``:416-420`` has
+its branches inverted (``zero_ij`` where the decay is >= 0.01, ``calc_ij`` — multiplying by a decay
+of 0 — elsewhere), so as written it leaves the ``tf.zeros`` ``cov_vv`` (``:337``) all zero.
+DESIGN.md §3 records the divergence.  ``taper_support`` is the non-zero
 pattern of one row of that covariance, from which the C4 kernels build Sigma's entries on the fly.
 """
 from __future__ import annotations
 
 import numpy as np
 
-TAPER_FLOOR = 0.01   # main_architecture_2_sampledistribution.py:392, :417
+TAPER_FLOOR = 0.01   # main_architecture_2_sampledistribution.py:392 (decay_fn's floor)
 TF_JITTER = 1e-6     # snippets_a2.py:161-163 (diagonal of the conditioning block)
 TF_SMALL = 1e-7      # snippets_a2.py:480 (|nom| or |denom| below -> delta = 0)
 
