@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--no-vgp", action="store_true", help="skip the C3 / C5 VGP training lines")
     p.add_argument("--no-c2", action="store_true", help="skip the C2 assembly + potrf line")
     p.add_argument("--vgp-steps", type=int, default=10)
+    p.add_argument("--vgp-mixed", action="store_true",
+                   help="also time C5 with the fp32 factor + fp64 refinement (slower than fp64 at "
+                        "M = 1,024 on MI355X, DESIGN.md §8)")
     p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 exact algorithm 3) line")
     p.add_argument("--c4-steps", type=int, default=10)
     p.add_argument("--no-sweep", action="store_true",
@@ -68,7 +71,7 @@ def parse():
                    help="per-run C4 kernel bytes from rocprofv3 PMC passes (tools/pmc_c4.py)")
     p.add_argument("--rank-check", action="store_true",
                    help="(tests) every rank prints its rank / world size and exits before any GPU call")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r4.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r5.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
 
@@ -169,6 +172,13 @@ def cpu_baseline(args, N):
                    f"{t_inc:.1f} s; the GPU line is at N={N}, where the O(N^3) init alone is "
                    f"{(N / n_inc) ** 3:.0f}x this sample's"),
         "gpu_same_sample": gpu_same,
+        # the headline's own config is N = 65,536, where the sample's dominant O(N^3) Cholesky +
+        # inverse grows by (N / n)^3 (the O(N^2) rounds by (N / n)^2): the sample's rate divided
+        # by that factor bounds the CPU's rate at the config from ABOVE (timing it there would take
+        # an hour of host time)
+        "at_config_upper_bound": {
+            "value": args.k / (t_inc * (N / n_inc) ** 3), "unit": "placements/s", "N": N,
+            "model": f"sample time x (N / {n_inc})^3"},
         "reference_algorithm": {
             "value": args.cpu_k / t_pinv, "unit": "placements/s",
             "sample": (f"pinv restatement of placement_algorithm2.placement_algorithm_2 on a "
@@ -886,8 +896,9 @@ def main():
     vgp = None
     if not args.no_vgp:
         kw = dict(world=world, rank=rank, barrier=barrier, maxtime=maxtime)
-        vgp = {"vgp_c3": vgp_line(args, "c3", **kw), "vgp_c5": vgp_line(args, "c5", **kw),
-               "vgp_c5_mixed": vgp_line(args, "c5", precision="mixed:2", **kw)}
+        vgp = {"vgp_c3": vgp_line(args, "c3", **kw), "vgp_c5": vgp_line(args, "c5", **kw)}
+        if args.vgp_mixed:  # (retired from the default line: DESIGN.md §8 item 3)
+            vgp["vgp_c5_mixed"] = vgp_line(args, "c5", precision="mixed:2", **kw)
     splits = splits_line(args, world, barrier, maxtime, rank) if world > 1 and not args.no_splits \
         else None
 

@@ -49,6 +49,18 @@ constexpr int CG_SEG = 16;  // lanes per diamond row of the 7-point CG walk (64:
 constexpr int CG_RPW = 64 / CG_SEG;  // diamond rows per wave
 constexpr int SEL_THREADS = 1024;
 
+// Pick t as the window re-score sees it: grid coordinates, point, and its CG column (box origin
+// and element offset of its slot).  Written by the first kernel that stages pick t (the window /
+// rows kernel of round t), so later rounds stage picks 0 .. t - 1 with ONE level of contiguous
+// loads instead of picks -> X and slot_of_round -> boxlo chains.
+struct PickRec {
+  int g[3];
+  int pad;
+  double x[3];
+  long long lo[3];
+  long long base;
+};
+
 struct ExactWS {
   double* coef;       // [n][m]: coef[i][0] diagonal (S_ii + eps), coef[i][1 + o] = S(i, i + off_o)
   double* bval;       // [nblk]
@@ -68,8 +80,11 @@ struct ExactWS {
   double* part_rr;    // [CG_B][CG_BLOCKS]
   double* rr;         // [CG_B][maxit + 2] residual norms per iteration
   int* cgstate;       // [CG_B][4]: done flag, iterations of the last solve
-  double* LS;         // [kmax][kmax] chol(S_AA + eps I)
-  double* LQ;         // [kmax][kmax] chol(Q_AA)
+  double* LS;         // chol(S_AA + eps I), packed lower triangle (row r at r (r + 1) / 2)
+  double* LQ;         // chol(Q_AA), packed likewise
+  double* RS;         // [kmax]: 1 / diag(LS)
+  double* RQ;         // [kmax]: 1 / diag(LQ)
+  struct PickRec* prec;  // [kmax]: what a re-score needs of pick t (grid point, box), see PickRec
   double* Qcols;      // [nslots][bv]: Q e_c on candidate c's box (zero outside it)
   int* slot_of_round; // [kmax]: the column slot of pick t
   unsigned char* qexact;  // [n]: 1 = qdiag[y] is Q_yy; 0 = an upper bound from the K_lo-step
@@ -149,8 +164,11 @@ static ExactWS exact_layout(void* base, int64_t I0, int64_t I1, int64_t I2, int 
   w.part_rr = (double*)take(8 * CG_BLOCKS * CG_B);
   w.rr = (double*)take(8 * (CG_MAXIT + 2) * CG_B);
   w.cgstate = (int*)take(16 * CG_B);
-  w.LS = (double*)take(8 * (size_t)kmax * kmax);
-  w.LQ = (double*)take(8 * (size_t)kmax * kmax);
+  w.LS = (double*)take(8 * (size_t)kmax * (kmax + 1) / 2);
+  w.LQ = (double*)take(8 * (size_t)kmax * (kmax + 1) / 2);
+  w.RS = (double*)take(8 * (size_t)kmax);
+  w.RQ = (double*)take(8 * (size_t)kmax);
+  w.prec = (PickRec*)take(sizeof(PickRec) * (size_t)kmax);
   w.Qcols = (double*)take(8 * (size_t)exact_slots(kmax) * bv);
   w.slot_of_round = (int*)take(4 * (size_t)kmax);
   w.qexact = (unsigned char*)take((size_t)n);
@@ -648,18 +666,23 @@ __device__ __forceinline__ double group_sum(double v) {
   return v;
 }
 
+// One fp64 LDS load from a 32-bit LDS byte address.
+__device__ __forceinline__ double lds_f64(unsigned addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) double*>((size_t)addr);
+}
+
 // bounds_cg with G candidates per wave: candidate g of the wave on lanes [g LPC, (g + 1) LPC),
 // reach-table node j = s LPC + l on slot s of group lane l (T <= 64 nodes, so G slots per lane).
 // The wave-uniform part of a CG step (the two reductions, three divisions, the Radau update) is
 // then ONE instruction stream for G candidates instead of one per candidate, and the reductions
 // are log2(LPC) intra-row steps.  pl: the group's 64 + 1 LDS doubles (the last one 0: the
-// neighbour of a node outside the table).
+// neighbour of a node outside the table); nba: the LDS byte addresses of each node's six
+// neighbours in pl (fixed for the kernel, so a gather is one ds_read with no address VALU).
 template <int G>
-__device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const unsigned (&nbo)[G][3],
+__device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const unsigned (&nba)[G][6],
                                                 double* pl, const int* cntl, int K, double hi_scale,
                                                 double mu, int l) {
   constexpr int LPC = 64 / G;
-  const char* plb = reinterpret_cast<const char*>(pl);
   double r[G], p[G], q[G];
 #pragma unroll
   for (int s = 0; s < G; ++s) {
@@ -680,10 +703,7 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
       if (s * LPC < cnt) {
         double acc = c[s][0] * p[s];
 #pragma unroll
-        for (int o = 0; o < 6; ++o) {
-          const unsigned off = (nbo[s][o >> 1] >> (16 * (o & 1))) & 0xffffu;
-          acc = fma(c[s][1 + o], *reinterpret_cast<const double*>(plb + off), acc);
-        }
+        for (int o = 0; o < 6; ++o) acc = fma(c[s][1 + o], lds_f64(nba[s][o]), acc);
         q[s] = s * LPC + l < cnt ? acc : 0.0;
         pq = fma(p[s], q[s], pq);
       }
@@ -721,9 +741,13 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
 // The all-candidate bounds of exact_bounds_reg_kernel<1, 6> (7-point stencil, reach table of
 // T <= 64 nodes: K <= 3) with G candidates per wave (bounds_cg_grp): G consecutive candidates
 // y .. y + G - 1 share most of their coefficient rows, so their loads meet in L1 / L2.
-#ifndef VGPOSP_BND_G
-#define VGPOSP_BND_G 8
+// Candidates per wave: 2 and 4 measured 0.94-0.96 ms per 128^3 K = 3 pass against 1.41 ms for one
+// (exact_bounds_reg_kernel<1, 6>), 8 spilled to AGPRs at one wave per SIMD (2.1 ms)
+// (profiles/r5_c4_bounds_grouped.jsonl)
+#ifndef VGPOSP_BND_G  // (A/B builds only)
+#define VGPOSP_BND_G 2
 #endif
+constexpr int BND_G = VGPOSP_BND_G;
 template <int G>
 __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
@@ -746,16 +770,16 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
   double* pl = plds[wave][gl];
   if (l == 0) pl[64] = 0.0;
   __syncthreads();
-  // node j = s LPC + l: its neighbours' byte offsets into pl, two per register, and its table
-  // offset as three signed bytes (-1: beyond the table)
-  unsigned nbo[G][3];
+  // node j = s LPC + l: its neighbours' LDS byte addresses in pl, and its table offset as three
+  // signed bytes (-1: beyond the table)
+  const unsigned plb = (unsigned)(size_t)(__attribute__((address_space(3))) void*)pl;
+  unsigned nba[G][6];
   int ofr[G];
 #pragma unroll
   for (int s = 0; s < G; ++s) {
     const int j = s * LPC + l;
 #pragma unroll
-    for (int o = 0; o < 3; ++o)
-      nbo[s][o] = (8u * (unsigned)nbl[j * M1 + 2 * o]) | ((8u * (unsigned)nbl[j * M1 + 2 * o + 1]) << 16);
+    for (int o = 0; o < 6; ++o) nba[s][o] = plb + 8u * (unsigned)nbl[j * M1 + o];
     ofr[s] = j < T ? ((offl[3 * j] + 128) | ((offl[3 * j + 1] + 128) << 8) |
                       ((offl[3 * j + 2] + 128) << 16))
                    : -1;
@@ -786,7 +810,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
       }
       load_coef_row<M>(coef, gi, c[s]);
     }
-    const double ub = bounds_cg_grp<G>(c, nbo, pl, cntl, K, hi_scale, mu, l);
+    const double ub = bounds_cg_grp<G>(c, nba, pl, cntl, K, hi_scale, mu, l);
     if (live && l == 0) qhi[y] = ub;
   }
 }
@@ -1561,43 +1585,45 @@ __device__ unsigned int g_exact_dbg_n;
 #define DBG_END(kind)
 #endif
 
-// Rows of chol(Q_AA) / chol(S_AA + eps I): in the workspace (row stride kmax) or packed lower
-// triangles staged in LDS (row r at r (r + 1) / 2).
+// Rows of chol(Q_AA) / chol(S_AA + eps I) as packed lower triangles (row r at r (r + 1) / 2), in
+// the workspace or staged in LDS, with the reciprocals of their diagonals.
 struct FactorRows {
   const double* lq;
   const double* ls;
-  int stride;  // > 0: row stride; 0: packed
-  __device__ __forceinline__ int at(int r, int s) const {
-    return stride ? r * stride + s : r * (r + 1) / 2 + s;
-  }
+  const double* rq;  // 1 / diag
+  const double* rs;
+  __device__ __forceinline__ int at(int r, int s) const { return r * (r + 1) / 2 + s; }
 };
 
-__device__ __forceinline__ FactorRows global_rows(const ExactWS& w, int km) {
-  return FactorRows{w.LQ, w.LS, km};
+__device__ __forceinline__ FactorRows global_rows(const ExactWS& w) {
+  return FactorRows{w.LQ, w.LS, w.RQ, w.RS};
 }
 
-// Stage rows 0 .. nr-1 of both factors as packed lower triangles into sm (2 nr (nr + 1) / 2
-// doubles), the whole workgroup.
-// (LQ's packed rows at sm, LS's at sm + ROWS_LDS / 2, so a row appended later lands in place;
-// nr (nr + 1) <= ROWS_LDS)
-__device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int km, int nr, double* sm) {
+// LDS of the staged rows: LQ's packed rows at sm, LS's at sm + ROWS_LDS / 2 (a row appended later
+// lands in place; nr (nr + 1) <= ROWS_LDS), the reciprocal diagonals after them.
+struct RowsLds {
+  double rows[ROWS_LDS];
+  double rq[EX_KMAX];
+  double rs[EX_KMAX];
+};
+
+// Stage rows 0 .. nr-1 of both factors and their reciprocal diagonals: contiguous copies (the
+// workspace holds them packed), the whole workgroup.  The caller synchronises before use.
+__device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int nr, RowsLds& sm) {
   const int np = nr * (nr + 1) / 2;
-  for (int e = threadIdx.x; e < 2 * np; e += blockDim.x) {
-    const int which = e >= np, k = which ? e - np : e;
-    int r = (int)((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
-    while (r * (r + 1) / 2 > k) --r;
-    while ((r + 1) * (r + 2) / 2 <= k) ++r;
-    const int s = k - r * (r + 1) / 2;
-    sm[which ? ROWS_LDS / 2 + k : k] = (which ? w.LS : w.LQ)[(size_t)r * km + s];
+  for (int e = threadIdx.x; e < np; e += blockDim.x) {
+    sm.rows[e] = w.LQ[e];
+    sm.rows[ROWS_LDS / 2 + e] = w.LS[e];
   }
-  __syncthreads();
-  return FactorRows{sm, sm + ROWS_LDS / 2, 0};
+  for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+    sm.rq[r] = w.RQ[r];
+    sm.rs[r] = w.RS[r];
+  }
+  return FactorRows{sm.rows, sm.rows + ROWS_LDS / 2, sm.rq, sm.rs};
 }
 
-// What a re-score needs of pick r, staged in LDS once per workgroup: its grid coordinates and
-// point, and where its CG column lives (box origin, element offset of its slot).  Read straight
-// from the workspace, sigma_off / qcol_at cost three to four DEPENDENT global loads per lane
-// (picks -> X, slot_of_round -> boxlo -> Qcols) on the critical path of every round.
+// What a re-score needs of pick r, staged in LDS once per workgroup (the PickRec fields as
+// arrays).
 struct StagedPicks {
   int g[EX_KMAX][3];
   double x[EX_KMAX][3];
@@ -1605,23 +1631,38 @@ struct StagedPicks {
   long long base[EX_KMAX];
 };
 
-// Picks 0 .. nA-1 (the whole workgroup calls it; the caller synchronises before use).
+// Picks 0 .. nA-1 (the whole workgroup calls it; the caller synchronises before use).  Picks
+// 0 .. nA-2 come from the workspace's pick records; pick nA-1 (this round's) is derived from
+// picks / X / slot_of_round / boxlo and, by workgroup 0, recorded for the rounds after.
 __device__ __forceinline__ void stage_picks(const EArgs& a, const ExactWS& w,
                                             const long long* picks, int nA, StagedPicks& sp) {
   const long long bv = w.b0 * w.b1 * w.b2;
   for (int r = threadIdx.x; r < nA; r += blockDim.x) {
-    const long long i = picks[r];
-    const int slot = w.slot_of_round[r];
-    sp.g[r][0] = (int)(i / (a.I1 * a.I2));
-    sp.g[r][1] = (int)((i / a.I2) % a.I1);
-    sp.g[r][2] = (int)(i % a.I2);
-    sp.x[r][0] = a.X[3 * i];
-    sp.x[r][1] = a.X[3 * i + 1];
-    sp.x[r][2] = a.X[3 * i + 2];
-    sp.lo[r][0] = w.boxlo[3 * slot];
-    sp.lo[r][1] = w.boxlo[3 * slot + 1];
-    sp.lo[r][2] = w.boxlo[3 * slot + 2];
-    sp.base[r] = (long long)slot * bv;
+    PickRec pr;
+    if (r + 1 < nA) {
+      pr = w.prec[r];
+    } else {
+      const long long i = picks[r];
+      const int slot = w.slot_of_round[r];
+      pr.g[0] = (int)(i / (a.I1 * a.I2));
+      pr.g[1] = (int)((i / a.I2) % a.I1);
+      pr.g[2] = (int)(i % a.I2);
+      pr.pad = 0;
+      pr.x[0] = a.X[3 * i];
+      pr.x[1] = a.X[3 * i + 1];
+      pr.x[2] = a.X[3 * i + 2];
+      pr.lo[0] = w.boxlo[3 * slot];
+      pr.lo[1] = w.boxlo[3 * slot + 1];
+      pr.lo[2] = w.boxlo[3 * slot + 2];
+      pr.base = (long long)slot * bv;
+      if (blockIdx.x == 0) w.prec[r] = pr;
+    }
+    for (int d = 0; d < 3; ++d) {
+      sp.g[r][d] = pr.g[d];
+      sp.x[r][d] = pr.x[d];
+      sp.lo[r][d] = pr.lo[d];
+    }
+    sp.base[r] = pr.base;
   }
 }
 
@@ -1664,11 +1705,8 @@ __device__ __forceinline__ double qcol_staged(const ExactWS& w, const StagedPick
   return w.Qcols[sp.base[r] + (l0 * w.b1 + l1) * w.b2 + l2];
 }
 
-// The cached delta of candidate y given the first nA picks, one wave: nominator
-// s_yy - |LS^-1 s_Ay|^2, P = qyy - |LQ^-1 q_Ay|^2.  Lane s holds the forward-substitution
-// unknowns z_s and z_{s+64}; every lane returns the delta.  sp: the picks staged in LDS
-// (stage_picks) or nullptr (read from the workspace).
 // The right-hand sides of a re-score: lane s holds s_{a_s y} and q_{a_s y} (and s + 64's).
+// sp: the picks staged in LDS (stage_picks) or nullptr (read from the workspace).
 struct RescoreVals {
   double vs0, vq0, vs1, vq1;
 };
@@ -1702,47 +1740,92 @@ __device__ __forceinline__ RescoreVals wave_rescore_vals(const EArgs& a, const E
   return RescoreVals{vs0, vq0, vs1, vq1};
 }
 
-// The forward substitutions of a re-score from its right-hand sides (rows 0 .. nA - 1 of L).
-template <int KIND>
-__device__ double wave_rescore_subst(const EArgs& a, const FactorRows& L, int nA, double qyy,
-                                     bool exact, const RescoreVals& v) {
+// The forward substitutions of a re-score, z = L^-1 v for both factors at once, column by column:
+// lane s holds the running right-hand sides b_s (and b_{s+64}); at row r the unknown
+// z_r = b_r / L_rr (times the staged reciprocal) is ONE wave-uniform value read from lane r, added
+// into the running sums of squares in row order, kept on lane r, and removed from the rows below
+// (b_s -= L_sr z_r on lanes r < s < rlim).  The chain per row is a lane read, a multiply and an
+// FMA, where the row-oriented form (a wave sum per row) took two butterflies and a division.
+struct Subst {
+  double bs0, bq0, bs1, bq1;  // right-hand sides, then (lane r < done) z_r
+  double ns, nq;              // sum of z_r^2 over the rows done, in row order
+};
+
+__device__ __forceinline__ Subst subst_begin(const RescoreVals& v) {
+  return Subst{v.vs0, v.vq0, v.vs1, v.vq1, 0.0, 0.0};
+}
+
+// Rows [r0, r1), updating the right-hand sides of rows < rlim only.
+__device__ __forceinline__ void subst_rows(const FactorRows& L, int r0, int r1, int rlim, Subst& st) {
   const int lane = threadIdx.x & 63;
-  const double vs0 = v.vs0, vq0 = v.vq0, vs1 = v.vs1, vq1 = v.vq1;
-  double zs0 = 0.0, zq0 = 0.0, zs1 = 0.0, zq1 = 0.0;
-  for (int r = 0; r < nA; ++r) {
-    double ds = 0.0, dq = 0.0;
-    if (lane < r) {
-      ds = L.ls[L.at(r, lane)] * zs0;
-      dq = L.lq[L.at(r, lane)] * zq0;
-    }
-    if (lane + 64 < r) {
-      ds = fma(L.ls[L.at(r, lane + 64)], zs1, ds);
-      dq = fma(L.lq[L.at(r, lane + 64)], zq1, dq);
-    }
-    ds = wave_sum(ds);
-    dq = wave_sum(dq);
-    const double dls = L.ls[L.at(r, r)], dlq = L.lq[L.at(r, r)];
+  for (int r = r0; r < r1; ++r) {
+    const double zs = wave_bcast(r < 64 ? st.bs0 : st.bs1, r & 63) * L.rs[r];
+    const double zq = wave_bcast(r < 64 ? st.bq0 : st.bq1, r & 63) * L.rq[r];
+    st.ns = fma(zs, zs, st.ns);
+    st.nq = fma(zq, zq, st.nq);
     if (r < 64) {
       if (lane == r) {
-        zs0 = (vs0 - ds) / dls;
-        zq0 = (vq0 - dq) / dlq;
+        st.bs0 = zs;
+        st.bq0 = zq;
+      } else if (lane > r && lane < rlim) {
+        st.bs0 = fma(-L.ls[L.at(lane, r)], zs, st.bs0);
+        st.bq0 = fma(-L.lq[L.at(lane, r)], zq, st.bq0);
       }
     } else if (lane == r - 64) {
-      zs1 = (vs1 - ds) / dls;
-      zq1 = (vq1 - dq) / dlq;
+      st.bs1 = zs;
+      st.bq1 = zq;
+    }
+    if (lane + 64 > r && lane + 64 < rlim) {
+      st.bs1 = fma(-L.ls[L.at(lane + 64, r)], zs, st.bs1);
+      st.bq1 = fma(-L.lq[L.at(lane + 64, r)], zq, st.bq1);
     }
   }
-  const double ns = wave_sum(fma(zs0, zs0, zs1 * zs1));
-  const double nq = wave_sum(fma(zq0, zq0, zq1 * zq1));
-  return delta_from(sigma_diag<KIND>(a) - ns, qyy - nq, exact, a.jitter, a.thr);
+}
+
+// The last row R of the system, once rows 0 .. R-1 are done with rlim = R: its right-hand side
+// minus the dot product of row R with the z held on lanes 0 .. R-1 (one wave sum per factor).
+__device__ __forceinline__ void subst_last(const FactorRows& L, int R, Subst& st) {
+  const int lane = threadIdx.x & 63;
+  double ds = 0.0, dq = 0.0;
+  if (lane < R) {
+    ds = L.ls[L.at(R, lane)] * st.bs0;
+    dq = L.lq[L.at(R, lane)] * st.bq0;
+  }
+  if (lane + 64 < R) {
+    ds = fma(L.ls[L.at(R, lane + 64)], st.bs1, ds);
+    dq = fma(L.lq[L.at(R, lane + 64)], st.bq1, dq);
+  }
+  ds = wave_sum(ds);
+  dq = wave_sum(dq);
+  const double vs = wave_bcast(R < 64 ? st.bs0 : st.bs1, R & 63);
+  const double vq = wave_bcast(R < 64 ? st.bq0 : st.bq1, R & 63);
+  const double zs = (vs - ds) * L.rs[R], zq = (vq - dq) * L.rq[R];
+  st.ns = fma(zs, zs, st.ns);
+  st.nq = fma(zq, zq, st.nq);
+}
+
+// The whole system of nA rows, the one arithmetic every re-score uses (the window kernel runs the
+// same two parts on either side of its barrier): rows 0 .. nA-2 column by column, row nA-1 by its
+// dot product.
+__device__ __forceinline__ void subst_all(const FactorRows& L, int nA, Subst& st) {
+  if (nA <= 0) return;
+  subst_rows(L, 0, nA - 1, nA - 1, st);
+  subst_last(L, nA - 1, st);
+}
+
+template <int KIND>
+__device__ __forceinline__ double rescore_delta(const EArgs& a, double qyy, bool exact,
+                                                const Subst& st) {
+  return delta_from(sigma_diag<KIND>(a) - st.ns, qyy - st.nq, exact, a.jitter, a.thr);
 }
 
 template <int KIND>
 __device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRows& L,
                                const long long* picks, int nA, long long y, double qyy,
                                bool exact, const StagedPicks* sp = nullptr) {
-  const RescoreVals v = wave_rescore_vals<KIND>(a, w, picks, nA, y, sp);
-  return wave_rescore_subst<KIND>(a, L, nA, qyy, exact, v);
+  Subst st = subst_begin(wave_rescore_vals<KIND>(a, w, picks, nA, y, sp));
+  subst_all(L, nA, st);
+  return rescore_delta<KIND>(a, qyy, exact, st);
 }
 
 // Bounded-lazy path, after the CG columns of the batch (cands[j] in slots[j], j < nb): each Q_cc
@@ -1765,8 +1848,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_refine_end_kernel(EArgs a, 
     const long long c = cands[j];
     if (c < 0) continue;
     const double qcc = qslot_at(w, slots[j], c, a.I1, a.I2);
-    const double d = wave_rescore<KIND>(a, w, global_rows(w, a.kmax), picks, (int)w.lastA[c], c,
-                                        qcc, true);
+    const double d = wave_rescore<KIND>(a, w, global_rows(w), picks, (int)w.lastA[c], c, qcc, true);
     if (lane == 0) {
       qdiag[c] = qcc;
       w.qexact[c] = 1;
@@ -1804,8 +1886,8 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_tighten_end_kernel(EArgs a,
   const int nt = w.ctl[CTL_NT];
   for (int j = wave; j < nt; j += NWAVE) {
     const long long c = w.rt_cand[j];
-    const double d = wave_rescore<KIND>(a, w, global_rows(w, a.kmax), picks, (int)w.lastA[c], c,
-                                        qdiag[c], false);
+    const double d = wave_rescore<KIND>(a, w, global_rows(w), picks, (int)w.lastA[c], c, qdiag[c],
+                                        false);
     if (lane == 0) {
       w.qexact[c] = 2;
       cache[c] = d;
@@ -1825,21 +1907,14 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_tighten_end_kernel(EArgs a,
   }
 }
 
-// After q_t = Q e_{a_t}, part 1: row t of LQ = chol(Q_AA) and of LS = chol(S_AA + eps I) (one wave
-// each; the earlier rows staged in LDS when they fit, the right-hand sides computed by all lanes
-// at once, then one forward substitution with lane s holding z_s).
-
-// Row `round` of both factors, the whole workgroup (>= 128 threads) calling: waves 0 and 1 compute
-// (LQ / LS), every thread stages the earlier rows.
-// Row `round` of LQ (wave 0) / LS (wave 1) from the staged picks and rows 0 .. round - 1 in L:
-// written to the workspace, and with lds_rows (the staged packed rows, L.stride == 0) appended
-// there too.
+// After q_t = Q e_{a_t}: row t of LQ = chol(Q_AA) (wave 0) and of LS = chol(S_AA + eps I)
+// (wave 1) from the staged picks and rows 0 .. round - 1 in L, column-oriented like the re-scores
+// (subst_rows; lane r ends with z_r): written to the workspace with the diagonal's reciprocal and,
+// with lds (the staged rows of this workgroup), appended there too.
 template <int KIND>
 __device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const FactorRows& L,
-                             const StagedPicks& sp, double* lds_rows) {
+                             const StagedPicks& sp, RowsLds* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int km = a.kmax;
-  const double* Lm = wave == 0 ? L.lq : L.ls;
   // (the staged forms of qcol_at(w, round, picks[r]) and sigma_off(a, at, picks[r]))
   auto val = [&](int r) {
     const CandPoint c{sp.g[r][0], sp.g[r][1], sp.g[r][2], sp.x[r][0], sp.x[r][1], sp.x[r][2]};
@@ -1848,46 +1923,44 @@ __device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const 
   };
   const double v0 = lane <= round ? val(lane) : 0.0;
   const double v1 = lane + 64 <= round ? val(lane + 64) : 0.0;
-  double z0 = 0.0, z1 = 0.0;
-  for (int r = 0; r < round; ++r) {
-    double d = 0.0;
-    if (lane < r) d = Lm[L.at(r, lane)] * z0;
-    if (lane + 64 < r) d = fma(Lm[L.at(r, lane + 64)], z1, d);
-    d = wave_sum(d);
-    const double dl = Lm[L.at(r, r)];
-    if (r < 64) {
-      if (lane == r) z0 = (v0 - d) / dl;
-    } else if (lane == r - 64) {
-      z1 = (v1 - d) / dl;
-    }
-  }
-  const double nz = wave_sum(fma(z0, z0, z1 * z1));
-  double* Lw = (wave == 0 ? w.LQ : w.LS) + (size_t)round * km;
-  if (lane < round) Lw[lane] = z0;
-  if (lane + 64 < round) Lw[lane + 64] = z1;
-  // diagonal: sqrt(v_round - |z|^2), v_round held by lane round % 64
+  // both factors' rows through one Subst (the unused half mirrors the used one; the two waves
+  // differ only in which half they keep)
+  Subst st{v0, v0, v1, v1, 0.0, 0.0};
+  const FactorRows Lw{wave == 0 ? L.lq : L.ls, wave == 0 ? L.lq : L.ls, wave == 0 ? L.rq : L.rs,
+                      wave == 0 ? L.rq : L.rs};
+  subst_rows(Lw, 0, round, round, st);
   const double vr = wave_bcast(round < 64 ? v0 : v1, round & 63);
-  const double dg = sqrt(vr - nz);
-  if (lane == 0) Lw[round] = dg;
-  if (lds_rows) {
-    double* Ll = lds_rows + (wave == 0 ? 0 : ROWS_LDS / 2) + round * (round + 1) / 2;
-    if (lane < round) Ll[lane] = z0;
-    if (lane + 64 < round) Ll[lane + 64] = z1;
-    if (lane == 0) Ll[round] = dg;
+  const double dg = sqrt(vr - st.ns);
+  const double rdg = 1.0 / dg;
+  const int off = round * (round + 1) / 2;
+  double* Lg = (wave == 0 ? w.LQ : w.LS) + off;
+  if (lane < round) Lg[lane] = st.bs0;
+  if (lane + 64 < round) Lg[lane + 64] = st.bs1;
+  if (lane == 0) {
+    Lg[round] = dg;
+    (wave == 0 ? w.RQ : w.RS)[round] = rdg;
+  }
+  if (lds) {
+    double* Ll = lds->rows + (wave == 0 ? 0 : ROWS_LDS / 2) + off;
+    if (lane < round) Ll[lane] = st.bs0;
+    if (lane + 64 < round) Ll[lane + 64] = st.bs1;
+    if (lane == 0) {
+      Ll[round] = dg;
+      (wave == 0 ? lds->rq : lds->rs)[round] = rdg;
+    }
   }
 }
 
 template <int KIND>
 __device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
-                                  const long long* picks, double* sm) {
+                                  const long long* picks, RowsLds& sm) {
   const int wave = threadIdx.x >> 6;
-  const int km = a.kmax;
   const long long at = picks[round];
   if (at < 0) return;
   __shared__ StagedPicks sp;
   stage_picks(a, w, picks, round + 1, sp);
-  const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, km, round, sm)
-                                                        : (__syncthreads(), global_rows(w, km));
+  const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, round, sm) : global_rows(w);
+  __syncthreads();
   if (wave > 1) return;
   wave_new_row<KIND>(a, w, round, L, sp, nullptr);
 }
@@ -1896,7 +1969,7 @@ __device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
 template <int KIND>
 __global__ __launch_bounds__(128) void exact_rows_kernel(EArgs a, ExactWS w, int round,
                                                          const long long* picks) {
-  __shared__ double sm[ROWS_LDS];
+  __shared__ RowsLds sm;
   block_factor_rows<KIND>(a, w, round, picks, sm);
 }
 
@@ -1917,63 +1990,70 @@ __device__ __forceinline__ Window window_of(const EArgs& a, long long at) {
 }
 
 // Part 2: re-score the window of a_t (snippets_a3.py:190-303; candidates in A -> 0), one wave per
-// candidate; upper bounds where Q_yy is still only bounded.
+// candidate; upper bounds where Q_yy is still only bounded.  Six waves: 0 and 1 compute the pick's
+// own rows (row `round` of LQ and LS: every workgroup, the same values, so the same bits written to
+// the workspace), 2 .. 5 one window candidate each — their right-hand sides and the substitution
+// of rows 0 .. round-1 run WHILE the new rows are computed; after one barrier the last row.
+constexpr int WIN_CAND = 4;                     // window candidates per workgroup
+constexpr int WIN_T = 64 * (2 + WIN_CAND);      // threads per workgroup
+
 template <int KIND>
-__global__ __launch_bounds__(256) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
-                                                           double* cache, const unsigned char* sel,
-                                                           ExactWS w, int round,
-                                                           const long long* picks) {
-  __shared__ double sm[ROWS_LDS];
+__global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
+                                                             double* cache, const unsigned char* sel,
+                                                             ExactWS w, int round,
+                                                             const long long* picks) {
+  __shared__ RowsLds sm;
   __shared__ StagedPicks sp;
   DBG_DECL
   DBG_T(0)
   const long long at = picks[round];
   if (at < 0) return;
   const Window v = window_of(a, at);
-  // every candidate of the workgroup walks the same factor rows and picks: stage them once.  The
-  // pick's own rows (row `round` of LQ and LS) are computed HERE, by waves 0 and 1 of every
-  // workgroup (the same values, so the same bits written to the workspace), instead of by the
-  // single-workgroup step kernel before this launch: 9 us per round off the critical path
   const int nr = round + 1;
   stage_picks(a, w, picks, nr, sp);
   const bool lds = nr * (nr + 1) <= ROWS_LDS;
-  const FactorRows L = lds ? stage_rows(w, a.kmax, round, sm)
-                           : (__syncthreads(), global_rows(w, a.kmax));
-  // the candidate's right-hand sides need only the staged picks: loaded before the new row (whose
-  // chain they then overlap), the substitutions after it
+  const FactorRows L = lds ? stage_rows(w, round, sm) : global_rows(w);
+  __syncthreads();
   DBG_T(1)
-  const long long e = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wave = threadIdx.x >> 6;
+  if (wave < 2) {
+    wave_new_row<KIND>(a, w, round, L, sp, lds ? &sm : nullptr);
+    DBG_T(2)
+    DBG_T(3)
+    __syncthreads();
+    DBG_T(4)
+    DBG_T(5)
+    if (blockIdx.x == 0) {
+      DBG_END(3)
+    }
+    return;
+  }
+  const long long e = (long long)blockIdx.x * WIN_CAND + (wave - 2);
   const bool live = e < v.w0 * v.w1 * v.w2;
   const long long y = live ? ((v.lo0 + e / (v.w1 * v.w2)) * a.I1 + v.lo1 + (e / v.w2) % v.w1) *
                                      a.I2 + v.lo2 + e % v.w2
                            : 0;
   const bool picked = live && sel[y];
-  RescoreVals rv{0.0, 0.0, 0.0, 0.0};
+  Subst st{0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double qyy = 0.0;
   bool ex = false;
   if (live && !picked) {
-    rv = wave_rescore_vals<KIND>(a, w, picks, nr, y, &sp);
+    st = subst_begin(wave_rescore_vals<KIND>(a, w, picks, nr, y, &sp));
     qyy = qdiag[y];
     ex = w.qexact[y] == 1;
+    subst_rows(L, 0, round, round, st);  // rows of picks 0 .. round-1 (subst_all's first part)
   }
-  DBG_T(2)
-  if ((threadIdx.x >> 6) < 2) wave_new_row<KIND>(a, w, round, L, sp, lds ? sm : nullptr);
-  DBG_T(3)
-  __syncthreads();
-  DBG_T(4)
+  __syncthreads();  // the new rows are in place
   if (!live) return;
   if (picked) {
     if ((threadIdx.x & 63) == 0) cache[y] = 0.0;
     return;
   }
-  const double d = wave_rescore_subst<KIND>(a, L, nr, qyy, ex, rv);
+  subst_last(L, round, st);
+  const double d = rescore_delta<KIND>(a, qyy, ex, st);
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
-  }
-  DBG_T(5)
-  if (blockIdx.x == 0) {
-    DBG_END(3)
   }
 }
 
@@ -2104,18 +2184,199 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_window_keys_kernel(EArgs a,
   }
 }
 
+// The keys of the blocks a round changed — the window of the previous pick, which contains the
+// pick itself (cutoff >= 1; its block is added explicitly otherwise) — recomputed with every
+// global read issued up front: the superblock keys of the whole grid (for the arg-max) and the
+// block keys of every superblock the window touches (for its superblock keys) are loaded into LDS
+// while the window's cache entries are; the new block keys, superblock keys and the arg-max are
+// then computed from LDS.  Returns false (nothing done) when the window exceeds the LDS lists;
+// the caller then takes the global-memory path (block_window_keys + block_argmax).
+constexpr int SK_MAXSB = 16;   // touched superblocks held in LDS
+constexpr int SK_MAXNSB = 4096;  // superblocks of the grid held in LDS (n <= 2^28)
+
+struct StepLds {
+  double sval[SK_MAXNSB];
+  long long sidx[SK_MAXNSB];
+  double bval[SK_MAXSB][ESB];
+  long long bidx[SK_MAXSB][ESB];
+  long long blk[WK_LIST];
+  long long sb[SK_MAXSB];
+  int nb, ns, ok;
+};
+
+__device__ __forceinline__ int sb_slot(const StepLds& L, long long sb) {
+  for (int q = 0; q < L.ns; ++q)
+    if (L.sb[q] == sb) return q;
+  return -1;
+}
+
+__device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
+                                      const unsigned char* sel, const ExactWS& w, long long nblk,
+                                      long long nsb, long long at, StepLds& L) {
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63, nwave = blockDim.x >> 6;
+  if (nsb > SK_MAXNSB) return false;
+  // level 1: the grid's superblock keys; the distinct blocks / superblocks of the window (wave 0)
+  for (long long q = t; q < nsb; q += blockDim.x) {
+    L.sval[q] = w.sval[q];
+    L.sidx[q] = w.sidx[q];
+  }
+  if (wave == 0) {
+    const Window v = window_of(a, at);
+    const long long nrow = v.w0 * v.w1;
+    const long long ab = at / EB;
+    bool fits = nrow <= 63 && v.w2 <= EB;
+    long long blo = 0, bhi = -1;
+    if (fits && lane < nrow && v.w2 > 0) {
+      const long long y0 = ((v.lo0 + lane / v.w1) * a.I1 + v.lo1 + lane % v.w1) * a.I2 + v.lo2;
+      blo = y0 / EB;
+      bhi = (y0 + v.w2 - 1) / EB;
+    }
+    // the pick's own block, on lane 63 (the whole list when the window is empty: cutoff 0),
+    // unless a row already covers it
+    const bool covered = __ballot(lane < 63 && bhi >= 0 && ab >= blo && ab <= bhi) != 0;
+    if (fits && lane == 63) {
+      blo = ab;
+      bhi = covered ? ab - 1 : ab;
+    }
+    // distinct blocks: rows increase with the lane, so duplicates sit between neighbours
+    long long prev = __shfl_up(bhi, 1, 64);
+    if (lane == 0) prev = -1;
+    const long long own = lane == 63 ? blo : max(blo, prev + 1);
+    const int nbl = bhi >= own ? (int)(bhi - own + 1) : 0;
+    const int ib = wave_incl_scan(nbl);
+    for (int q = 0; q < nbl; ++q)
+      if (ib - nbl + q < WK_LIST) L.blk[ib - nbl + q] = own + q;
+    if (lane == 63) {
+      L.nb = ib;
+      L.ok = fits && ib <= 4 * nwave && ib <= WK_LIST;
+    }
+  }
+  __syncthreads();
+  if (!L.ok) return false;
+  const int nb = L.nb;
+  if (t == 0) {  // the distinct superblocks of the (sorted except the last) block list
+    int ns = 0;
+    for (int q = 0; q < nb; ++q) {
+      const long long sb = L.blk[q] / ESB;
+      bool seen = false;
+      for (int u = 0; u < ns; ++u) seen = seen || L.sb[u] == sb;
+      if (!seen) {
+        if (ns == SK_MAXSB) {
+          ns = SK_MAXSB + 1;
+          break;
+        }
+        L.sb[ns++] = sb;
+      }
+    }
+    L.ns = ns;
+  }
+  __syncthreads();
+  const int ns = L.ns;
+  if (ns > SK_MAXSB) return false;
+  // level 2: the touched superblocks' block keys into LDS, the window blocks' entries (registers)
+  for (int e = t; e < ns * ESB; e += blockDim.x) {
+    const int q = e / ESB, j = e % ESB;
+    const long long b = L.sb[q] * ESB + j;
+    L.bval[q][j] = b < nblk ? w.bval[b] : 0.0;
+    L.bidx[q][j] = b < nblk ? w.bidx[b] : -1;
+  }
+  constexpr int PER = EB / 64;
+  double c[4][PER];
+  unsigned char sl[4][PER];
+  long long mine[4];
+  int cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = wave + q * nwave;
+    mine[q] = j < nb ? L.blk[j] : -1;
+    cnt += j < nb;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const long long y = mine[q] >= 0 ? mine[q] * EB + e * 64 + lane : a.n;
+      c[q][e] = y < a.n ? cache[y] : 0.0;
+      sl[q][e] = y < a.n ? sel[y] : 1;
+    }
+  }
+  __syncthreads();  // the LDS block keys are in place before the new ones overwrite them
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= cnt) break;
+    Key k{0ull, 0ull};
+#pragma unroll
+    for (int e = 0; e < PER; ++e)
+      key_take_max(k, key_enc(c[q][e], sl[q][e] ? -1 : mine[q] * EB + e * 64 + lane));
+    k = wave_keymax(k);
+    if (lane == 0) {
+      const double kv = key_value(k);
+      const long long ki = key_index(k);
+      w.bval[mine[q]] = kv;
+      w.bidx[mine[q]] = ki;
+      const int qs = sb_slot(L, mine[q] / ESB);
+      L.bval[qs][mine[q] % ESB] = kv;
+      L.bidx[qs][mine[q] % ESB] = ki;
+    }
+  }
+  __syncthreads();
+  for (int q = wave; q < ns; q += nwave) {
+    double v = L.bval[q][lane];
+    long long idx = L.bidx[q][lane];
+    wave_keymax(v, idx);
+    if (lane == 0) {
+      w.sval[L.sb[q]] = v;
+      w.sidx[L.sb[q]] = idx;
+      L.sval[L.sb[q]] = v;
+      L.sidx[L.sb[q]] = idx;
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+// Workgroup-wide arg-max over the superblock keys staged in LDS (block_argmax's reduction).
+__device__ long long block_argmax_lds(const StepLds& L, long long nsb) {
+  __shared__ double sv[SEL_THREADS / 64];
+  __shared__ long long si[SEL_THREADS / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double v = 0.0;
+  long long idx = -1;
+  for (long long s = t; s < nsb; s += SEL_THREADS) {
+    if (L.sidx[s] >= 0 && key_gt(L.sval[s], L.sidx[s], v, idx)) {
+      v = L.sval[s];
+      idx = L.sidx[s];
+    }
+  }
+  wave_keymax(v, idx);
+  if (lane == 0) {
+    sv[wave] = v;
+    si[wave] = idx;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    v = lane < SEL_THREADS / 64 ? sv[lane] : 0.0;
+    idx = lane < SEL_THREADS / 64 ? si[lane] : -1;
+    wave_keymax(v, idx);
+    if (lane == 0) si[0] = idx;
+  }
+  __syncthreads();
+  const long long r = si[0];
+  __syncthreads();
+  return r;
+}
+
 // One round of the bounded-lazy rounds, decided on the device (vgposp_exact_steps).  First the
-// keys of the previous round's window (its re-scored cache entries), then the arg-max of the
-// cache; if its Q_yy is exact (a refined candidate, its CG column in a slot) it is picked (marked
-// selected, its cache entry 0, its keys refreshed) and, with `rows`, the pick's rows of
-// chol(Q_AA) and chol(S_AA + eps I) are appended; otherwise the round STALLS: ctl[STALL] = round,
-// and the B best cache entries that have no column yet become the pending refinement batch
+// keys of the blocks the previous round changed (its pick and its window's re-scored entries),
+// then the arg-max of the cache; if its Q_yy is exact (a refined candidate, its CG column in a
+// slot) it is picked (marked selected, its cache entry 0; its keys are refreshed by the next
+// round's kernel, the first reader — its window contains it) and, with `rows`, the pick's rows
+// of chol(Q_AA) and chol(S_AA + eps I) are appended; otherwise the round STALLS: ctl[STALL] =
+// round, and the B best cache entries that have no column yet become the pending refinement batch
 // (rf_cand / rf_slot, ctl[NB]), each given a free slot or the oldest unpinned one — the host
 // loop's rule (sparse_placement.ExactWindowGreedy.run_bounded, round 3).  Every later kernel of
 // the issued rounds sees the stall (picks[round] stays -1, ctl[STALL] >= 0) and does nothing,
 // until the host has run the refinement (exact_refine_end_kernel clears the stall) and re-issues
 // the rounds from the stalled one.  One workgroup; a round is this kernel plus the window
-// re-score (exact_window_kernel).
+// re-score (exact_window_kernel).  A stalled round refreshed the keys of round - 1's pick first,
+// so the stall / refinement kernels that run next see current keys.
 template <int KIND>
 __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, double* cache,
                                                                  unsigned char* sel, ExactWS w,
@@ -2124,15 +2385,28 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
                                                                  int rows, long long* picks,
                                                                  double* pick_delta) {
   __shared__ int s_slot;
-  __shared__ double sm[ROWS_LDS];
+  __shared__ union {
+    StepLds k;
+    RowsLds r;
+  } sm;
   DBG_DECL
   DBG_T(0)
   if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
   const long long n = ea.n;
-  if (round > 0 && picks[round - 1] >= 0)
-    block_window_keys(ea, cache, sel, w, nblk, picks[round - 1]);
-  DBG_T(1)
-  const long long a = block_argmax(w, nsb);
+  long long a;
+  const long long prev = round > 0 ? picks[round - 1] : -1;
+  if (prev >= 0 && block_window_keys_lds(ea, cache, sel, w, nblk, nsb, prev, sm.k)) {
+    DBG_T(1)
+    a = block_argmax_lds(sm.k, nsb);
+  } else {
+    if (prev >= 0) {  // (a window too large for the LDS lists; the pick's own block as well)
+      block_window_keys(ea, cache, sel, w, nblk, prev);
+      if (threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, prev);
+      __syncthreads();
+    }
+    DBG_T(1)
+    a = block_argmax(w, nsb);
+  }
   DBG_T(2)
   if (threadIdx.x == 0) s_slot = -1;
   __syncthreads();
@@ -2155,9 +2429,8 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
       }
     }
     __syncthreads();
-    if (a >= 0 && threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, a);
     DBG_T(4)
-    if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm);
+    if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm.r);
     DBG_T(5)
     DBG_END(2)
     return;
@@ -2419,7 +2692,7 @@ int exact_update_t(const EArgs& a, const double* qdiag, double* cache, unsigned 
     VG_LAUNCH_CHECK();
   }
   if (nw > 0) {
-    hipLaunchKernelGGL(exact_window_kernel<KIND>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, s,
+    hipLaunchKernelGGL(exact_window_kernel<KIND>, dim3((unsigned)ceil_div(nw, WIN_CAND)), dim3(WIN_T), 0, s,
                        a, qdiag, cache, sel, w, round, picks);
     VG_LAUNCH_CHECK();
   }
@@ -2569,8 +2842,8 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
     VG_LAUNCH_CHECK();                                                                           \
     return 0;                                                                                    \
   }
-  if (a.m1 == 6 && T <= 64 && VGPOSP_BND_G > 1) {  // K <= 3: G candidates per wave
-    constexpr int G = VGPOSP_BND_G;
+  if (a.m1 == 6 && T <= 64 && BND_G > 1) {  // K <= 3: G candidates per wave
+    constexpr int G = BND_G;
     const unsigned gblocks =
         (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES * G), 8LL),
                                            BND_GRID / 8));
@@ -2627,7 +2900,7 @@ extern "C" int vgposp_exact_steps(VGPOSP_EXACT_PARAMS, int round0, int round1, i
       }
       if (more && nw > 0) {  // the window of pick r (no-op when the round stalled: picks[r] = -1)
         ProfScope ps("exact_update", s, 0.0, 0.0);
-        hipLaunchKernelGGL(exact_window_kernel<KD>, dim3((unsigned)ceil_div(nw, 4)), dim3(256), 0, s,
+        hipLaunchKernelGGL(exact_window_kernel<KD>, dim3((unsigned)ceil_div(nw, WIN_CAND)), dim3(WIN_T), 0, s,
                            a, qdiag, cache, selected, w, r, pk);
         VG_LAUNCH_CHECK();
       }
