@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 5, call E: the step kernel's superblock dedupe parallelised, the substitution's factor
+# loads pipelined, one reciprocal per bounds CG step: C4 GPU tests, the 128^3 run against lib_bnda2
+# (previous rounds and bounds chain) and lib_bndr4 (4 candidates per wave), stamps.
+set -e
+R=${GRAFT_REPO_ROOT:-$PWD}
+O=$R/gpurun_out/r5e
+mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_exact.py tests/test_gpu_alg3_golden.py tests/test_gpu_sharded.py -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+echo ok tests
+for rep in 1 2 3; do
+  for v in product bnda2 bndr4; do
+    if [ $v = product ]; then L=$R/vgposp_amd/libvgposp.so; else L=$R/tools/variants/lib_$v.so; fi
+    VGPOSP_LIB=$L timeout -k 10 120 python -u tools/c4_time.py --reps 10 32 \
+      | sed "s/^{/{\"variant\": \"$v\", \"rep\": $rep, /" >> $O/c4_ab.jsonl
+  done
+done
+echo ok c4 ab
+VGPOSP_LIB=$R/tools/variants/lib_dbg.so timeout -k 10 120 python -u tools/exact_dbg.py > $O/c4_dbg.json 2>&1
+echo ok dbg

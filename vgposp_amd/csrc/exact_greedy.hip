@@ -693,7 +693,11 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double rr = 1.0, g = 0.0, gmu = mu > 0.0 ? 1.0 / mu : 0.0;
+  // the Gauss-Radau recursion in projective form, gamma^mu = N / D (radau_step without its
+  // division: gamma - alpha = (N - alpha D) / D, so N' = N - alpha D, D' = mu N' + delta D), and
+  // alpha = rr / pq, delta = beta = rn / rr from ONE reciprocal of pq rr per step: the division
+  // chain that every candidate pair's wave runs drops from three divisions per step to one
+  double rr = 1.0, g = 0.0, gN = 1.0, gD = mu;
   for (int it = 0; it < K; ++it) {
     const int cnt = cntl[it + 1];
     double pq = 0.0;
@@ -709,7 +713,8 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
       }
     }
     pq = group_sum<LPC>(pq);
-    const double alpha = rr / pq;
+    const double inv = 1.0 / (pq * rr);
+    const double alpha = rr * rr * inv;
     g = fma(alpha, rr, g);
     if (it + 1 == K && mu <= 0.0) break;
     double rn = 0.0;
@@ -719,8 +724,11 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
       rn = fma(r[s], r[s], rn);
     }
     rn = group_sum<LPC>(rn);
-    const double beta = rn / rr;  // = delta_{k+1}
-    if (mu > 0.0) gmu = radau_step(gmu, alpha, mu, beta);
+    const double beta = rn * pq * inv;  // = rn / rr = delta_{k+1}
+    if (mu > 0.0) {
+      gN = fma(-alpha, gD, gN);
+      gD = fma(mu, gN, beta * gD);
+    }
     rr = rn;
     if (it + 1 == K) break;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -735,7 +743,7 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  return bound_value(g, gmu, rr, mu, hi_scale);
+  return bound_value(g, mu > 0.0 ? gN / gD : 0.0, rr, mu, hi_scale);
 }
 
 // The all-candidate bounds of exact_bounds_reg_kernel<1, 6> (7-point stencil, reach table of
@@ -1586,17 +1594,25 @@ __device__ unsigned int g_exact_dbg_n;
 #endif
 
 // Rows of chol(Q_AA) / chol(S_AA + eps I) as packed lower triangles (row r at r (r + 1) / 2), in
-// the workspace or staged in LDS, with the reciprocals of their diagonals.
-struct FactorRows {
-  const double* lq;
-  const double* ls;
-  const double* rq;  // 1 / diag
-  const double* rs;
+// the workspace (P = const double*) or staged in LDS (P = an address-space-3 pointer, so the
+// substitutions' loads are ds_reads: through a generic pointer they were flat loads, which the
+// compiler must drain with vmcnt(0) AND lgkmcnt(0) before every use, exposing each row's load
+// latency on the chain), with the reciprocals of their diagonals.
+typedef const __attribute__((address_space(3))) double* lds_cdptr;
+
+template <class P>
+struct FRows {
+  P lq;
+  P ls;
+  P rq;  // 1 / diag
+  P rs;
   __device__ __forceinline__ int at(int r, int s) const { return r * (r + 1) / 2 + s; }
 };
+typedef FRows<const double*> GRows;
+typedef FRows<lds_cdptr> LRows;
 
-__device__ __forceinline__ FactorRows global_rows(const ExactWS& w) {
-  return FactorRows{w.LQ, w.LS, w.RQ, w.RS};
+__device__ __forceinline__ GRows global_rows(const ExactWS& w) {
+  return GRows{w.LQ, w.LS, w.RQ, w.RS};
 }
 
 // LDS of the staged rows: LQ's packed rows at sm, LS's at sm + ROWS_LDS / 2 (a row appended later
@@ -1609,7 +1625,7 @@ struct RowsLds {
 
 // Stage rows 0 .. nr-1 of both factors and their reciprocal diagonals: contiguous copies (the
 // workspace holds them packed), the whole workgroup.  The caller synchronises before use.
-__device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int nr, RowsLds& sm) {
+__device__ __forceinline__ LRows stage_rows(const ExactWS& w, int nr, RowsLds& sm) {
   const int np = nr * (nr + 1) / 2;
   for (int e = threadIdx.x; e < np; e += blockDim.x) {
     sm.rows[e] = w.LQ[e];
@@ -1619,7 +1635,8 @@ __device__ __forceinline__ FactorRows stage_rows(const ExactWS& w, int nr, RowsL
     sm.rq[r] = w.RQ[r];
     sm.rs[r] = w.RS[r];
   }
-  return FactorRows{sm.rows, sm.rows + ROWS_LDS / 2, sm.rq, sm.rs};
+  return LRows{(lds_cdptr)sm.rows, (lds_cdptr)(sm.rows + ROWS_LDS / 2), (lds_cdptr)sm.rq,
+               (lds_cdptr)sm.rs};
 }
 
 // What a re-score needs of pick r, staged in LDS once per workgroup (the PickRec fields as
@@ -1755,36 +1772,49 @@ __device__ __forceinline__ Subst subst_begin(const RescoreVals& v) {
   return Subst{v.vs0, v.vq0, v.vs1, v.vq1, 0.0, 0.0};
 }
 
-// Rows [r0, r1), updating the right-hand sides of rows < rlim only.
-__device__ __forceinline__ void subst_rows(const FactorRows& L, int r0, int r1, int rlim, Subst& st) {
+// Rows [r0, r1), updating the right-hand sides of rows < rlim only.  Branch-free: every lane
+// computes its update and selects (the same values the predicated form stores).  Column r + 1's
+// factor entries are loaded while row r is eliminated, unconditionally
+// (the last iteration re-reads column r1 - 1) so the count of loads in flight is static and the
+// compiler can wait for the older ones only; a lane at or beyond rlim reads row rlim - 1's entry
+// (in bounds, unused).
+template <class R>
+__device__ __forceinline__ void subst_rows(const R& L, int r0, int r1, int rlim, Subst& st) {
+  if (r0 >= r1 || rlim <= 0) return;
   const int lane = threadIdx.x & 63;
+  const int l0 = min(lane, rlim - 1), l1 = min(lane + 64, rlim - 1);
+  double cs0 = L.ls[L.at(l0, r0)], cq0 = L.lq[L.at(l0, r0)];
+  double cs1 = L.ls[L.at(l1, r0)], cq1 = L.lq[L.at(l1, r0)];
+  // each lane's own rows' reciprocal diagonals, in registers: lane r forms z_r = b_r / L_rr
+  // itself (the same multiply), so the chain reads no LDS for it
+  const double rs0 = L.rs[l0], rq0 = L.rq[l0], rs1 = L.rs[l1], rq1 = L.rq[l1];
   for (int r = r0; r < r1; ++r) {
-    const double zs = wave_bcast(r < 64 ? st.bs0 : st.bs1, r & 63) * L.rs[r];
-    const double zq = wave_bcast(r < 64 ? st.bq0 : st.bq1, r & 63) * L.rq[r];
+    const int rn = min(r + 1, r1 - 1);
+    const double ns0 = L.ls[L.at(l0, rn)], nq0 = L.lq[L.at(l0, rn)];
+    const double ns1 = L.ls[L.at(l1, rn)], nq1 = L.lq[L.at(l1, rn)];
+    const double zs = wave_bcast(r < 64 ? st.bs0 * rs0 : st.bs1 * rs1, r & 63);
+    const double zq = wave_bcast(r < 64 ? st.bq0 * rq0 : st.bq1 * rq1, r & 63);
     st.ns = fma(zs, zs, st.ns);
     st.nq = fma(zq, zq, st.nq);
-    if (r < 64) {
-      if (lane == r) {
-        st.bs0 = zs;
-        st.bq0 = zq;
-      } else if (lane > r && lane < rlim) {
-        st.bs0 = fma(-L.ls[L.at(lane, r)], zs, st.bs0);
-        st.bq0 = fma(-L.lq[L.at(lane, r)], zq, st.bq0);
-      }
-    } else if (lane == r - 64) {
-      st.bs1 = zs;
-      st.bq1 = zq;
-    }
-    if (lane + 64 > r && lane + 64 < rlim) {
-      st.bs1 = fma(-L.ls[L.at(lane + 64, r)], zs, st.bs1);
-      st.bq1 = fma(-L.lq[L.at(lane + 64, r)], zq, st.bq1);
-    }
+    const bool own0 = lane == r, own1 = lane + 64 == r;
+    const bool up0 = lane > r && lane < rlim, up1 = lane + 64 > r && lane + 64 < rlim;
+    const double us0 = fma(-cs0, zs, st.bs0), uq0 = fma(-cq0, zq, st.bq0);
+    const double us1 = fma(-cs1, zs, st.bs1), uq1 = fma(-cq1, zq, st.bq1);
+    st.bs0 = own0 ? zs : (up0 ? us0 : st.bs0);
+    st.bq0 = own0 ? zq : (up0 ? uq0 : st.bq0);
+    st.bs1 = own1 ? zs : (up1 ? us1 : st.bs1);
+    st.bq1 = own1 ? zq : (up1 ? uq1 : st.bq1);
+    cs0 = ns0;
+    cq0 = nq0;
+    cs1 = ns1;
+    cq1 = nq1;
   }
 }
 
 // The last row R of the system, once rows 0 .. R-1 are done with rlim = R: its right-hand side
 // minus the dot product of row R with the z held on lanes 0 .. R-1 (one wave sum per factor).
-__device__ __forceinline__ void subst_last(const FactorRows& L, int R, Subst& st) {
+template <class RT>
+__device__ __forceinline__ void subst_last(const RT& L, int R, Subst& st) {
   const int lane = threadIdx.x & 63;
   double ds = 0.0, dq = 0.0;
   if (lane < R) {
@@ -1807,7 +1837,8 @@ __device__ __forceinline__ void subst_last(const FactorRows& L, int R, Subst& st
 // The whole system of nA rows, the one arithmetic every re-score uses (the window kernel runs the
 // same two parts on either side of its barrier): rows 0 .. nA-2 column by column, row nA-1 by its
 // dot product.
-__device__ __forceinline__ void subst_all(const FactorRows& L, int nA, Subst& st) {
+template <class R>
+__device__ __forceinline__ void subst_all(const R& L, int nA, Subst& st) {
   if (nA <= 0) return;
   subst_rows(L, 0, nA - 1, nA - 1, st);
   subst_last(L, nA - 1, st);
@@ -1819,8 +1850,8 @@ __device__ __forceinline__ double rescore_delta(const EArgs& a, double qyy, bool
   return delta_from(sigma_diag<KIND>(a) - st.ns, qyy - st.nq, exact, a.jitter, a.thr);
 }
 
-template <int KIND>
-__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const FactorRows& L,
+template <int KIND, class R>
+__device__ double wave_rescore(const EArgs& a, const ExactWS& w, const R& L,
                                const long long* picks, int nA, long long y, double qyy,
                                bool exact, const StagedPicks* sp = nullptr) {
   Subst st = subst_begin(wave_rescore_vals<KIND>(a, w, picks, nA, y, sp));
@@ -1911,8 +1942,8 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_tighten_end_kernel(EArgs a,
 // (wave 1) from the staged picks and rows 0 .. round - 1 in L, column-oriented like the re-scores
 // (subst_rows; lane r ends with z_r): written to the workspace with the diagonal's reciprocal and,
 // with lds (the staged rows of this workgroup), appended there too.
-template <int KIND>
-__device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const FactorRows& L,
+template <int KIND, class R>
+__device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const R& L,
                              const StagedPicks& sp, RowsLds* lds) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // (the staged forms of qcol_at(w, round, picks[r]) and sigma_off(a, at, picks[r]))
@@ -1926,7 +1957,7 @@ __device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const 
   // both factors' rows through one Subst (the unused half mirrors the used one; the two waves
   // differ only in which half they keep)
   Subst st{v0, v0, v1, v1, 0.0, 0.0};
-  const FactorRows Lw{wave == 0 ? L.lq : L.ls, wave == 0 ? L.lq : L.ls, wave == 0 ? L.rq : L.rs,
+  const R Lw{wave == 0 ? L.lq : L.ls, wave == 0 ? L.lq : L.ls, wave == 0 ? L.rq : L.rs,
                       wave == 0 ? L.rq : L.rs};
   subst_rows(Lw, 0, round, round, st);
   const double vr = wave_bcast(round < 64 ? v0 : v1, round & 63);
@@ -1941,12 +1972,13 @@ __device__ void wave_new_row(const EArgs& a, const ExactWS& w, int round, const 
     (wave == 0 ? w.RQ : w.RS)[round] = rdg;
   }
   if (lds) {
-    double* Ll = lds->rows + (wave == 0 ? 0 : ROWS_LDS / 2) + off;
+    __attribute__((address_space(3))) double* Ll =
+        (__attribute__((address_space(3))) double*)(lds->rows + (wave == 0 ? 0 : ROWS_LDS / 2) + off);
     if (lane < round) Ll[lane] = st.bs0;
     if (lane + 64 < round) Ll[lane + 64] = st.bs1;
     if (lane == 0) {
       Ll[round] = dg;
-      (wave == 0 ? lds->rq : lds->rs)[round] = rdg;
+      ((__attribute__((address_space(3))) double*)(wave == 0 ? lds->rq : lds->rs))[round] = rdg;
     }
   }
 }
@@ -1959,10 +1991,16 @@ __device__ void block_factor_rows(const EArgs& a, const ExactWS& w, int round,
   if (at < 0) return;
   __shared__ StagedPicks sp;
   stage_picks(a, w, picks, round + 1, sp);
-  const FactorRows L = round * (round + 1) <= ROWS_LDS ? stage_rows(w, round, sm) : global_rows(w);
-  __syncthreads();
-  if (wave > 1) return;
-  wave_new_row<KIND>(a, w, round, L, sp, nullptr);
+  if (round * (round + 1) <= ROWS_LDS) {
+    const LRows L = stage_rows(w, round, sm);
+    __syncthreads();
+    if (wave > 1) return;
+    wave_new_row<KIND>(a, w, round, L, sp, nullptr);
+  } else {
+    __syncthreads();
+    if (wave > 1) return;
+    wave_new_row<KIND>(a, w, round, global_rows(w), sp, nullptr);
+  }
 }
 
 
@@ -1997,27 +2035,21 @@ __device__ __forceinline__ Window window_of(const EArgs& a, long long at) {
 constexpr int WIN_CAND = 4;                     // window candidates per workgroup
 constexpr int WIN_T = 64 * (2 + WIN_CAND);      // threads per workgroup
 
-template <int KIND>
-__global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
-                                                             double* cache, const unsigned char* sel,
-                                                             ExactWS w, int round,
-                                                             const long long* picks) {
-  __shared__ RowsLds sm;
-  __shared__ StagedPicks sp;
+// The window kernel after its staging barrier: waves 0 and 1 the pick's new rows, 2 .. 5 one
+// window candidate each (R: the rows in LDS or in the workspace).
+template <int KIND, class R>
+__device__ __forceinline__ void window_tail(const EArgs& a, const double* __restrict__ qdiag,
+                                            double* cache, const unsigned char* sel,
+                                            const ExactWS& w, int round, const long long* picks,
+                                            const Window& v, const StagedPicks& sp, const R& L,
+                                            RowsLds* lds) {
   DBG_DECL
-  DBG_T(0)
-  const long long at = picks[round];
-  if (at < 0) return;
-  const Window v = window_of(a, at);
   const int nr = round + 1;
-  stage_picks(a, w, picks, nr, sp);
-  const bool lds = nr * (nr + 1) <= ROWS_LDS;
-  const FactorRows L = lds ? stage_rows(w, round, sm) : global_rows(w);
-  __syncthreads();
-  DBG_T(1)
   const int wave = threadIdx.x >> 6;
+  DBG_T(0)
+  DBG_T(1)
   if (wave < 2) {
-    wave_new_row<KIND>(a, w, round, L, sp, lds ? &sm : nullptr);
+    wave_new_row<KIND>(a, w, round, L, sp, lds);
     DBG_T(2)
     DBG_T(3)
     __syncthreads();
@@ -2054,6 +2086,28 @@ __global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const doub
   if ((threadIdx.x & 63) == 0) {
     cache[y] = d;
     w.lastA[y] = (unsigned char)(round + 1);
+  }
+}
+
+template <int KIND>
+__global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
+                                                             double* cache, const unsigned char* sel,
+                                                             ExactWS w, int round,
+                                                             const long long* picks) {
+  __shared__ RowsLds sm;
+  __shared__ StagedPicks sp;
+  const long long at = picks[round];
+  if (at < 0) return;
+  const Window v = window_of(a, at);
+  const int nr = round + 1;
+  stage_picks(a, w, picks, nr, sp);
+  if (nr * (nr + 1) <= ROWS_LDS) {
+    const LRows L = stage_rows(w, round, sm);
+    __syncthreads();
+    window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, L, &sm);
+  } else {
+    __syncthreads();
+    window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, global_rows(w), nullptr);
   }
 }
 
@@ -2199,16 +2253,11 @@ struct StepLds {
   long long sidx[SK_MAXNSB];
   double bval[SK_MAXSB][ESB];
   long long bidx[SK_MAXSB][ESB];
-  long long blk[WK_LIST];
+  long long blk[64];
+  int bslot[64];  // the superblock slot (index into sb) of each listed block
   long long sb[SK_MAXSB];
   int nb, ns, ok;
 };
-
-__device__ __forceinline__ int sb_slot(const StepLds& L, long long sb) {
-  for (int q = 0; q < L.ns; ++q)
-    if (L.sb[q] == sb) return q;
-  return -1;
-}
 
 __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
                                       const unsigned char* sel, const ExactWS& w, long long nblk,
@@ -2224,7 +2273,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     const Window v = window_of(a, at);
     const long long nrow = v.w0 * v.w1;
     const long long ab = at / EB;
-    bool fits = nrow <= 63 && v.w2 <= EB;
+    const bool fits = nrow <= 63 && v.w2 <= EB;
     long long blo = 0, bhi = -1;
     if (fits && lane < nrow && v.w2 > 0) {
       const long long y0 = ((v.lo0 + lane / v.w1) * a.I1 + v.lo1 + lane % v.w1) * a.I2 + v.lo2;
@@ -2244,35 +2293,46 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     const long long own = lane == 63 ? blo : max(blo, prev + 1);
     const int nbl = bhi >= own ? (int)(bhi - own + 1) : 0;
     const int ib = wave_incl_scan(nbl);
-    for (int q = 0; q < nbl; ++q)
-      if (ib - nbl + q < WK_LIST) L.blk[ib - nbl + q] = own + q;
-    if (lane == 63) {
-      L.nb = ib;
-      L.ok = fits && ib <= 4 * nwave && ib <= WK_LIST;
+    const int nbt = __builtin_amdgcn_readlane(ib, 63);
+    const bool ok = fits && nbt >= 1 && nbt <= 64 && nbt <= 4 * nwave;
+    if (ok)
+      for (int q = 0; q < nbl; ++q) L.blk[ib - nbl + q] = own + q;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the distinct superblocks, lane q for listed block q: the list is increasing except its last
+    // entry when that is the pick's block (not covered by a row), which joins an earlier entry's
+    // superblock if one shares it
+    int ns = 0;
+    if (ok) {
+      const long long bq = lane < nbt ? L.blk[lane] : -1;
+      const long long sq = bq >= 0 ? bq / ESB : -1;
+      long long sp = __shfl_up(sq, 1, 64);
+      const bool pick_last = !covered;
+      const long long spk = __shfl(sq, nbt - 1, 64);
+      const unsigned long long same = __ballot(lane < nbt - 1 && sq == spk);
+      bool isnew = lane < nbt && (lane == 0 || sp != sq);
+      if (pick_last && lane == nbt - 1) isnew = same == 0;
+      const int in = wave_incl_scan(isnew ? 1 : 0);
+      ns = __builtin_amdgcn_readlane(in, 63);
+      int slot = in - 1;
+      if (pick_last && same != 0) {
+        const int f = __builtin_ctzll(same);  // the first earlier entry in the pick's superblock
+        const int fs = __shfl(in, f, 64) - 1;
+        if (lane == nbt - 1) slot = fs;
+      }
+      if (isnew && in - 1 < SK_MAXSB) L.sb[in - 1] = sq;
+      if (lane < nbt) L.bslot[lane] = slot;
+    }
+    if (lane == 0) {
+      L.nb = nbt;
+      L.ns = ns;
+      L.ok = ok && ns <= SK_MAXSB;
     }
   }
   __syncthreads();
   if (!L.ok) return false;
-  const int nb = L.nb;
-  if (t == 0) {  // the distinct superblocks of the (sorted except the last) block list
-    int ns = 0;
-    for (int q = 0; q < nb; ++q) {
-      const long long sb = L.blk[q] / ESB;
-      bool seen = false;
-      for (int u = 0; u < ns; ++u) seen = seen || L.sb[u] == sb;
-      if (!seen) {
-        if (ns == SK_MAXSB) {
-          ns = SK_MAXSB + 1;
-          break;
-        }
-        L.sb[ns++] = sb;
-      }
-    }
-    L.ns = ns;
-  }
-  __syncthreads();
-  const int ns = L.ns;
-  if (ns > SK_MAXSB) return false;
+  const int nb = L.nb, ns = L.ns;
   // level 2: the touched superblocks' block keys into LDS, the window blocks' entries (registers)
   for (int e = t; e < ns * ESB; e += blockDim.x) {
     const int q = e / ESB, j = e % ESB;
@@ -2284,11 +2344,13 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
   double c[4][PER];
   unsigned char sl[4][PER];
   long long mine[4];
+  int mslot[4];
   int cnt = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int j = wave + q * nwave;
     mine[q] = j < nb ? L.blk[j] : -1;
+    mslot[q] = j < nb ? L.bslot[j] : 0;
     cnt += j < nb;
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
@@ -2311,9 +2373,8 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
       const long long ki = key_index(k);
       w.bval[mine[q]] = kv;
       w.bidx[mine[q]] = ki;
-      const int qs = sb_slot(L, mine[q] / ESB);
-      L.bval[qs][mine[q] % ESB] = kv;
-      L.bidx[qs][mine[q] % ESB] = ki;
+      L.bval[mslot[q]][mine[q] % ESB] = kv;
+      L.bidx[mslot[q]][mine[q] % ESB] = ki;
     }
   }
   __syncthreads();
