@@ -4,6 +4,8 @@ VGPOSP_LIB=$PWD/tools/variants/lib_dbg.so python tools/exact_dbg.py [--one-level
 Prints the mean phase durations (us) of the stall kernel and the step kernel over one 128^3 run:
 stall: argmax | top-B | slot staging | slot ranking | batch write;
 step: window keys | argmax | slot lookup | pick + key refresh | factor rows;
+--dbg2 (a -DVGPOSP_EXACT_DBG=2 build): the step kernel's key refresh instead — window list |
+level-2 loads | block keys | superblock keys | arg-max;
 window (workgroup 0, wave 0, which computes the new LQ row; from the end of the staging): - | new
 row | - | wait at the barrier for the candidates' waves | -."""
 import ctypes
@@ -29,7 +31,8 @@ buf = (ctypes.c_ulonglong * (64 * 8))()
 lib.vgposp_exact_dbg(buf)  # reset
 out = {}
 for kind, name, phases in ((1, "stall", ["argmax", "topb", "stage", "rank", "write"]),
-                           (2, "step", ["window_keys", "argmax", "slot", "pick_keys", "rows"]),
+                           (2, "step", ["list", "loads", "keys", "superkeys", "argmax"] if "--dbg2" in sys.argv
+                            else ["window_keys", "argmax", "slot", "pick_keys", "rows"]),
                            (3, "window", ["_", "new_row", "_", "barrier", "_"])):
     out[name] = {"phases": phases}
 run.run()

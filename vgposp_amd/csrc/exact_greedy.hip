@@ -364,6 +364,7 @@ __device__ __forceinline__ double bound_value(double g, double gmu, double rrK, 
 }
 
 constexpr int BND_GRID = 65536;  // workgroups of an all-candidate bounds launch, at most
+constexpr int BND_GRP_GRID = 16384;  // the same for the grouped kernel (exact_bounds_grp_kernel)
 constexpr int BND_T = 256;
 constexpr int BND_WAVES = BND_T / 64;
 constexpr int BND_SMAX = 14;
@@ -749,6 +750,26 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
 // The all-candidate bounds of exact_bounds_reg_kernel<1, 6> (7-point stencil, reach table of
 // T <= 64 nodes: K <= 3) with G candidates per wave (bounds_cg_grp): G consecutive candidates
 // y .. y + G - 1 share most of their coefficient rows, so their loads meet in L1 / L2.
+// Division of n < 2^31 by a divisor fixed for the launch, by multiply-high (Granlund-Montgomery,
+// the "round-up" form): q = (umulhi(n, m) + n) >> l with l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1.  Exhaustively checked on the host for the grid sizes used;
+// the candidate decode of the bounds pass spent ~60 instructions per candidate pair in two
+// generic 32-bit divisions.
+struct FastDiv {
+  unsigned m;
+  int l;
+};
+
+static FastDiv fast_div_for(unsigned d) {
+  int l = 0;
+  while ((1ull << l) < d) ++l;
+  return FastDiv{(unsigned)((((1ull << 32) * ((1ull << l) - d)) / d) + 1), l};
+}
+
+__device__ __forceinline__ unsigned fast_div(unsigned n, FastDiv f) {
+  return (__umulhi(n, f.m) + n) >> f.l;
+}
+
 // Candidates per wave: 2 and 4 measured 0.94-0.96 ms per 128^3 K = 3 pass against 1.41 ms for one
 // (exact_bounds_reg_kernel<1, 6>), 8 spilled to AGPRs at one wave per SIMD (2.1 ms)
 // (profiles/r5_c4_bounds_grouped.jsonl)
@@ -761,7 +782,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
     const int* __restrict__ tab_off, const int* __restrict__ tab_nb,
     const int* __restrict__ tab_cnt, int T, int K, double hi_scale, double mu, long long c0,
-    long long c1, double* __restrict__ qhi) {
+    long long c1, double* __restrict__ qhi, FastDiv div12, FastDiv div2) {
   constexpr int LPC = 64 / G, M1 = 6, M = 7;
   __shared__ double plds[BND_WAVES][G][65];
   __shared__ short nbl[64 * M1];
@@ -803,8 +824,8 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
     const long long y = yb + gl;
     const bool live = y < xhi;
     const unsigned yu = (unsigned)(live ? y : yb);
-    const int y0 = (int)(yu / I12), yr = (int)(yu - (unsigned)y0 * I12);
-    const int y1 = yr / I2i, y2 = yr - y1 * I2i;
+    const int y0 = (int)fast_div(yu, div12), yr = (int)(yu - (unsigned)y0 * I12);
+    const int y1 = (int)fast_div((unsigned)yr, div2), y2 = yr - y1 * I2i;
     double c[G][M];
 #pragma unroll
     for (int s = 0; s < G; ++s) {
@@ -1421,6 +1442,60 @@ __device__ __forceinline__ void wave_topb(double (&v)[P], long long (&id)[P], in
   }
 }
 
+// The exact top B of the n = 64 Q items staged in LDS (sv / si), one wave, by rank: item k's rank
+// is the number of items with a greater key (a strict total order: keys carry distinct indices),
+// so items of rank < B land at ov / oi[rank] in the order B wave arg-maxes would extract them;
+// if fewer than B items are real, slot nreal gets the empty key (value 0, index -1), which ends the
+// list.  Lane l holds items l Q .. l Q + Q - 1; taken (bit q): its item q was among the B.  The
+// encoded keys are staged in kv_s / ki_s first, then every lane compares its items against all n
+// broadcast LDS reads with no serial dependency — where B successive wave arg-maxes (each a
+// six-step cross-lane reduction) were a serial chain of B.
+template <int Q>
+__device__ __forceinline__ void wave_rank_topb(const double* sv, const long long* si, int B,
+                                               unsigned long long* kv_s, unsigned long long* ki_s,
+                                               double* ov, long long* oi, int& taken) {
+  const int lane = threadIdx.x & 63;
+  constexpr int N = 64 * Q;
+  unsigned long long mv[Q], mi[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int k = lane * Q + q;
+    const Key e = key_enc(sv[k], si[k]);
+    mv[q] = e.v;
+    mi[q] = e.i;
+    kv_s[k] = e.v;
+    ki_s[k] = e.i;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int rank[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) rank[q] = 0;
+  for (int j = 0; j < N; ++j) {
+    const Key o{kv_s[j], ki_s[j]};
+#pragma unroll
+    for (int q = 0; q < Q; ++q) rank[q] += key_enc_gt(o, Key{mv[q], mi[q]}) ? 1 : 0;
+  }
+  taken = 0;
+  int real = 0;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const bool live = mv[q] != 0ull;
+    real += live ? 1 : 0;
+    if (live && rank[q] < B) {
+      ov[rank[q]] = key_value(Key{mv[q], mi[q]});
+      oi[rank[q]] = key_index(Key{mv[q], mi[q]});
+      taken |= 1 << q;
+    }
+  }
+  real = (int)wave_sum((double)real);
+  if (lane == 0 && real < B) {
+    ov[real] = 0.0;
+    oi[real] = -1;
+  }
+}
+
 // The B best of `count` items (key(i, v, idx), i < count <= P * SEL_THREADS) -> out[0] = how many
 // (<= B), out[1 ..] = their indices, best first.  sv / si: LDS scratch [16 B].  Whole workgroup.
 constexpr int TOPW = 8;  // block_topb_keys' first pass: each wave's best TOPW
@@ -1462,7 +1537,10 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
         id1[q] = si[lane * Q1 + q];
       }
       int tk = 0;
-      wave_topb<Q1>(v1, id1, B, sv + NW * CG_B, si + NW * CG_B, &tk);
+      __shared__ unsigned long long s_kv[NW * TOPW], s_ki[NW * TOPW];
+      (void)v1;
+      (void)id1;
+      wave_rank_topb<Q1>(sv, si, B, s_kv, s_ki, sv + NW * CG_B, si + NW * CG_B, tk);
       const unsigned long long m0 = __ballot(tk & 1), m1 = __ballot(tk & 2);
       int full = 0;
 #pragma unroll
@@ -1591,6 +1669,11 @@ __device__ unsigned int g_exact_dbg_n;
 #define DBG_DECL
 #define DBG_T(k)
 #define DBG_END(kind)
+#endif
+#if VGPOSP_EXACT_DBG == 1
+#define DBG_END_STEP() DBG_END(2)
+#else
+#define DBG_END_STEP()
 #endif
 
 // Rows of chol(Q_AA) / chol(S_AA + eps I) as packed lower triangles (row r at r (r + 1) / 2), in
@@ -2261,7 +2344,11 @@ struct StepLds {
 
 __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
                                       const unsigned char* sel, const ExactWS& w, long long nblk,
-                                      long long nsb, long long at, StepLds& L) {
+                                      long long nsb, long long at, StepLds& L,
+                                      unsigned long long* dt = nullptr) {
+  // (dt: debug builds with VGPOSP_EXACT_DBG=2 stamp the phases here)
+#define DBG_PT(k) \
+  if (dt != nullptr && threadIdx.x == 0) dt[k] = __builtin_amdgcn_s_memrealtime();
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, nwave = blockDim.x >> 6;
   if (nsb > SK_MAXNSB) return false;
   // level 1: the grid's superblock keys; the distinct blocks / superblocks of the window (wave 0)
@@ -2331,6 +2418,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     }
   }
   __syncthreads();
+  DBG_PT(1)
   if (!L.ok) return false;
   const int nb = L.nb, ns = L.ns;
   // level 2: the touched superblocks' block keys into LDS, the window blocks' entries (registers)
@@ -2360,6 +2448,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     }
   }
   __syncthreads();  // the LDS block keys are in place before the new ones overwrite them
+  DBG_PT(2)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (q >= cnt) break;
@@ -2378,6 +2467,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     }
   }
   __syncthreads();
+  DBG_PT(3)
   for (int q = wave; q < ns; q += nwave) {
     double v = L.bval[q][lane];
     long long idx = L.bidx[q][lane];
@@ -2390,6 +2480,8 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     }
   }
   __syncthreads();
+  DBG_PT(4)
+#undef DBG_PT
   return true;
 }
 
@@ -2456,9 +2548,21 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
   const long long n = ea.n;
   long long a;
   const long long prev = round > 0 ? picks[round - 1] : -1;
-  if (prev >= 0 && block_window_keys_lds(ea, cache, sel, w, nblk, nsb, prev, sm.k)) {
+#if VGPOSP_EXACT_DBG == 2
+  unsigned long long* dtp = dbg_t;
+#else
+  unsigned long long* dtp = nullptr;
+#endif
+  if (prev >= 0 && block_window_keys_lds(ea, cache, sel, w, nblk, nsb, prev, sm.k, dtp)) {
+#if VGPOSP_EXACT_DBG != 2
     DBG_T(1)
+#endif
     a = block_argmax_lds(sm.k, nsb);
+#if VGPOSP_EXACT_DBG == 2
+    DBG_T(5)
+    DBG_END(2)
+    (void)0;
+#endif
   } else {
     if (prev >= 0) {  // (a window too large for the LDS lists; the pick's own block as well)
       block_window_keys(ea, cache, sel, w, nblk, prev);
@@ -2493,7 +2597,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
     DBG_T(4)
     if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm.r);
     DBG_T(5)
-    DBG_END(2)
+    DBG_END_STEP()
     return;
   }
   // stall: the batch is chosen by exact_stall_kernel, which the host launches first thing in
@@ -2905,11 +3009,15 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
   }
   if (a.m1 == 6 && T <= 64 && BND_G > 1) {  // K <= 3: G candidates per wave
     constexpr int G = BND_G;
+    // at most 16,384 workgroups: each wave then walks ~16 candidate pairs and the per-workgroup
+    // table staging and per-wave address setup are amortised (65,536: 0.84 ms per 128^3 pass,
+    // 16,384: 0.76, 8,192: 0.77; profiles/r5_c4_ab.jsonl)
     const unsigned gblocks =
         (unsigned)(8 * std::min<long long>(ceil_div(ceil_div(waves, BND_WAVES * G), 8LL),
-                                           BND_GRID / 8));
+                                           BND_GRP_GRID / 8));
     hipLaunchKernelGGL(exact_bounds_grp_kernel<G>, dim3(gblocks), dim3(BND_T), 0, s, w.coef, a.I0,
-                       a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0, lc1, out);
+                       a.I1, a.I2, tab_off, tab_nb, tab_cnt, T, K, hi_scale, mu, lc0, lc1, out,
+                       fast_div_for((unsigned)(a.I1 * a.I2)), fast_div_for((unsigned)a.I2));
     VG_LAUNCH_CHECK();
     return 0;
   }
