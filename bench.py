@@ -67,7 +67,7 @@ def parse():
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                         "the multi-rank path on one GPU with VGPOSP_BENCH_DEVICE=0)")
-    p.add_argument("--c4-pmc", default=os.path.join(ROOT, "profiles", "pmc_c4_r4.json"),
+    p.add_argument("--c4-pmc", default=os.path.join(ROOT, "profiles", "pmc_c4_r5.json"),
                    help="per-run C4 kernel bytes from rocprofv3 PMC passes (tools/pmc_c4.py)")
     p.add_argument("--rank-check", action="store_true",
                    help="(tests) every rank prints its rank / world size and exits before any GPU call")
@@ -936,12 +936,7 @@ def main():
     elif dom == "gemm_f64":
         roof["traffic_note"] = (
             "null: no PMC pass of this build in " + os.path.relpath(args.traffic, ROOT) +
-            ". Round 4's FETCH_SIZE pass over this step died inside rocprofv3's counter-collection "
-            "dispatch hook (SIGSEGV on the first copy_leaf_kernel launch of the factorization, "
-            "profiles/r4_rocprof_pmc_final_segv.log; the un-profiled step and the kernel-trace "
-            "pass run the same path). The GEMM kernel body is unchanged since round 3, whose "
-            "pass measured 2.07 GB per launch (profiles/traffic_r3.json, tied to round 3's "
-            "sources).")
+            " (tools/step65k.cpp + tools/pmc_traffic.py measure one: DESIGN.md §5)")
     # the HBM-bound kernel of the placement rounds, with its PMC-measured traffic
     ms_t, n_t, _, by_t = prof["greedy_trmv"]
     hbm = {"kernel": "greedy_trmv", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,

@@ -114,3 +114,94 @@ __global__ __launch_bounds__(BT_T) void exact_bounds_tile_kernel(
 
 // Round 0 (snippets_a3.py:77-124): A empty, nom = s_yy, denom = 1 / Q_yy - eps (an upper bound of
 // the delta where qexact[y] = 0).
+
+// exact_cg_wg_kernel (round 5): the whole CG solve of a column in ONE workgroup of 1,024 threads
+// (part A / part B as workgroup phases, their sums workgroup reductions): one launch per batch
+// instead of 2 per iteration.  Parity green (75 C4 GPU tests), but one CU per column cannot
+// stream the column's late iterations: exact_cg 1.46 -> 4.0 ms per 128^3 run
+// (profiles/r5_c4_ab.jsonl, call k).  Constants and launch it used:
+//
+// constexpr int CG_WG = 1024;
+//   hipLaunchKernelGGL(exact_cg_wg_kernel<true>, dim3((unsigned)nb), dim3(CG_WG), 0, s, w, a.I0,
+//                      a.I1, a.I2, a.offs, a.m1, radius, slots, centers, cg_iters, tol2);
+//
+// // The whole CG solve of column j = blockIdx.x in ONE workgroup of CG_WG threads: iteration it's
+// // part A (p_it on the fly, q = (S + eps I) p_it, p.q) and part B (x, r, |r|^2) are the per-phase
+// // kernels' node arithmetic, their sums workgroup reductions in a fixed order (deterministic), and
+// // the barrier inside each reduction orders the phases.  No launch per phase: the batch's columns
+// // run side by side on CG_B CUs for all iterations.  The same stopping rule and state as the
+// // per-phase kernels (state[0] = 1, state[1] = it when |r_it|^2 <= tol2 at the top of iteration it).
+// template <bool OCT>
+// __global__ __launch_bounds__(CG_WG) void exact_cg_wg_kernel(ExactWS w, long long I0, long long I1,
+//                                                            long long I2, const int* offs, int m1,
+//                                                            int srad, const int* slots,
+//                                                            const long long* centers, int cg_iters,
+//                                                            double tol2) {
+//   __shared__ double red[CG_WG / 64];
+//   const int j = blockIdx.x;
+//   const CGCol cc = cg_col(w, j);
+//   if (cc.state[0]) return;  // no candidate in this column of the batch
+//   const int slot = slots[j];
+//   const long long a = centers[j];
+//   double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
+//   const int m = m1 + 1;
+//   const int t = threadIdx.x, lane = t & 63;
+//   auto wg_sum = [&](double v) {
+//     v = wave_sum(v);
+//     if (lane == 0) red[t >> 6] = v;
+//     __syncthreads();
+//     double tot = 0.0;
+// #pragma unroll
+//     for (int i = 0; i < CG_WG / 64; ++i) tot += red[i];
+//     __syncthreads();
+//     return tot;
+//   };
+//   double rr = cc.rr[0], rr_prev = rr;
+//   for (int it = 0; it < cg_iters; ++it) {
+//     if (rr <= tol2) {
+//       if (t == 0) {
+//         cc.state[0] = 1;
+//         cc.state[1] = it;
+//       }
+//       return;
+//     }
+//     const double beta = it == 0 ? 0.0 : rr / rr_prev;
+//     const double* pold = (it & 1) ? cc.p0 : cc.p1;
+//     double* pnew = (it & 1) ? cc.p1 : cc.p0;
+//     const ActiveCube q = active_cube(w, I1, I2, slot, a, it, srad);
+//     double acc = 0.0;
+//     auto node_a = [&](long long g0, long long g1, long long g2) {
+//       const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
+//       const double pi = it == 0 ? cc.r[l] : fma(beta, pold[l], cc.r[l]);
+//       const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * coef_stride(m);
+//       double s = c[0] * pi;
+//       for (int o = 0; o < m1; ++o) {
+//         const double cv = c[1 + o];
+//         if (cv == 0.0) continue;
+//         const long long j0 = g0 + offs[3 * o] - q.lo0, j1 = g1 + offs[3 * o + 1] - q.lo1,
+//                         j2 = g2 + offs[3 * o + 2] - q.lo2;
+//         if (j0 < 0 || j0 >= w.b0 || j1 < 0 || j1 >= w.b1 || j2 < 0 || j2 >= w.b2) continue;
+//         const long long jj = (j0 * w.b1 + j1) * w.b2 + j2;
+//         const double pj = it == 0 ? cc.r[jj] : fma(beta, pold[jj], cc.r[jj]);
+//         s = fma(cv, pj, s);
+//       }
+//       pnew[l] = pi;
+//       cc.q[l] = s;
+//       acc = fma(pi, s, acc);
+//     };
+//     cg_walk<OCT>(w, q, I0, I1, I2, a, it, t, CG_WG, node_a);
+//     const double alpha = rr / wg_sum(acc);
+//     acc = 0.0;
+//     auto node_b = [&](long long g0, long long g1, long long g2) {
+//       const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
+//       x[l] = fma(alpha, pnew[l], x[l]);
+//       const double ri = fma(-alpha, cc.q[l], cc.r[l]);
+//       cc.r[l] = ri;
+//       acc = fma(ri, ri, acc);
+//     };
+//     cg_walk<OCT>(w, q, I0, I1, I2, a, it, t, CG_WG, node_b);
+//     rr_prev = rr;
+//     rr = wg_sum(acc);
+//     if (t == 0) cc.rr[it + 1] = rr;
+//   }
+// }

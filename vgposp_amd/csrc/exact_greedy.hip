@@ -1288,12 +1288,14 @@ __device__ __forceinline__ void diamond_row(long long rw, long long& d0, long lo
 // Visit the active nodes of iteration `it` (grid coordinates): the active cube, thread t its
 // t-th node; or (OCT) the Manhattan ball of radius it + 1 around the centre a, one wave per
 // diamond row, lane l the row's l-th node (rows longer than 64 nodes: l, l + 64, ...).
+// Thread `tid` of `nth` threads walking the region; waves take consecutive groups of CG_RPW
+// diamond rows.
 template <bool OCT, class F>
 __device__ __forceinline__ void cg_walk(const ExactWS& w, const ActiveCube& q, long long I0,
-                                        long long I1, long long I2, long long a, int it, F&& f) {
+                                        long long I1, long long I2, long long a, int it,
+                                        long long tid, long long nth, F&& f) {
   if (!OCT) {
-    for (long long t = (long long)blockIdx.x * CG_T + threadIdx.x; t < q.ne;
-         t += (long long)gridDim.x * CG_T) {
+    for (long long t = tid; t < q.ne; t += nth) {
       const long long g0 = q.c0 + t / (q.e1 * q.e2), g1 = q.c1 + (t / q.e2) % q.e1,
                       g2 = q.c2 + t % q.e2;
       f(g0, g1, g2);
@@ -1306,8 +1308,7 @@ __device__ __forceinline__ void cg_walk(const ExactWS& w, const ActiveCube& q, l
   // per wave left most lanes idle and quadrupled the waves of the late iterations)
   const int lane = threadIdx.x & 63, sub = lane / CG_SEG, sl = lane % CG_SEG;
   const long long nrows = diamond_rows(R);
-  for (long long rw = ((long long)blockIdx.x * (CG_T / 64) + (threadIdx.x >> 6)) * CG_RPW + sub;
-       rw < nrows; rw += (long long)gridDim.x * (CG_T / 64) * CG_RPW) {
+  for (long long rw = (tid >> 6) * CG_RPW + sub; rw < nrows; rw += (nth >> 6) * CG_RPW) {
     long long d0, d1;
     diamond_row(rw, d0, d1);
     const long long g0 = a0 + d0, g1 = a1 + d1;
@@ -1367,7 +1368,8 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
     cc.q[l] = s;
     acc = fma(pi, s, acc);
   };
-  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, node);
+  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, (long long)blockIdx.x * CG_T + threadIdx.x,
+               (long long)gridDim.x * CG_T, node);
   block_partial(acc, cc.part_pq, red);
 }
 
@@ -1394,7 +1396,8 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
     cc.r[l] = ri;
     acc = fma(ri, ri, acc);
   };
-  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, node);
+  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, (long long)blockIdx.x * CG_T + threadIdx.x,
+               (long long)gridDim.x * CG_T, node);
   block_partial(acc, cc.part_rr, red);
 }
 
