@@ -205,3 +205,62 @@ __global__ __launch_bounds__(BT_T) void exact_bounds_tile_kernel(
 //     if (t == 0) cc.rr[it + 1] = rr;
 //   }
 // }
+
+// exact_window_kernel<KIND, STEP = true> (round 5): round r's window kernel at 14 candidates per
+// 1,024-thread workgroup whose LAST workgroup (a ticket in ctl[8] after a device-scope fence)
+// runs round r + 1's step (step_body, exact_step_kernel's code): one launch per round.  Parity
+// green (75 C4 GPU tests), but slower (profiles/r5_c4_ab.jsonl, call m): the 16-wave window
+// workgroups alone cost 0.69 -> 0.98 ms per run, the fences and the ticket another 0.14 ms
+// (4.04 -> 4.64 ms).  The host loop skipped the standalone step of a round whose step had run
+// in the previous window launch.
+//
+// struct WinSm {
+//   RowsLds r;
+// };
+//
+// // STEP: the last workgroup to finish (a ticket in ctl[CTL_TICKET], after a device-scope fence of
+// // every workgroup's stores) then runs round + 1's step (step_body) — one launch per round instead
+// // of two.  The step's arithmetic is exact_step_kernel's.
+// template <int KIND, bool STEP>
+// __global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
+//                                                              double* cache, unsigned char* sel,
+//                                                              ExactWS w, int round, long long* picks,
+//                                                              long long nblk, long long nsb,
+//                                                              int nslots, double* pick_delta) {
+//   __shared__ typename std::conditional<STEP, StepSm, WinSm>::type sm;
+//   __shared__ StagedPicks sp;
+//   __shared__ int s_slot, s_last;
+//   const long long at = picks[round];
+//   if (at < 0) {  // stalled (the step returns at once) or nothing left to pick
+//     if constexpr (STEP) {
+//       if (blockIdx.x == 0)
+//         step_body<KIND>(a, cache, sel, w, nblk, nsb, nslots, round + 1, 0, picks, pick_delta, sm,
+//                         s_slot);
+//     }
+//     return;
+//   }
+//   const Window v = window_of(a, at);
+//   const int nr = round + 1;
+//   stage_picks(a, w, picks, nr, sp);
+//   if (nr * (nr + 1) <= ROWS_LDS) {
+//     const LRows L = stage_rows(w, round, sm.r);
+//     __syncthreads();
+//     window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, L, &sm.r);
+//   } else {
+//     __syncthreads();
+//     window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, global_rows(w), nullptr);
+//   }
+//   if constexpr (STEP) {
+//     __threadfence();
+//     __syncthreads();
+//     if (threadIdx.x == 0) s_last = atomicAdd(w.ctl + CTL_TICKET, 1) == (int)gridDim.x - 1;
+//     __syncthreads();
+//     if (!s_last) return;
+//     __threadfence();
+//     if (threadIdx.x == 0) w.ctl[CTL_TICKET] = 0;
+//     step_body<KIND>(a, cache, sel, w, nblk, nsb, nslots, round + 1, 0, picks, pick_delta, sm,
+//                     s_slot);
+//   } else {
+//     (void)nblk, (void)nsb, (void)nslots, (void)pick_delta, (void)s_slot, (void)s_last;
+//   }
+// }

@@ -2114,14 +2114,17 @@ __device__ __forceinline__ Window window_of(const EArgs& a, long long at) {
 }
 
 // Part 2: re-score the window of a_t (snippets_a3.py:190-303; candidates in A -> 0), one wave per
-// candidate; upper bounds where Q_yy is still only bounded.  Six waves: 0 and 1 compute the pick's
+// candidate; upper bounds where Q_yy is still only bounded.  2 + WIN_CAND waves: 0 and 1 compute the pick's
 // own rows (row `round` of LQ and LS: every workgroup, the same values, so the same bits written to
-// the workspace), 2 .. 5 one window candidate each — their right-hand sides and the substitution
+// the workspace), the others one window candidate each — their right-hand sides and the substitution
 // of rows 0 .. round-1 run WHILE the new rows are computed; after one barrier the last row.
-constexpr int WIN_CAND = 4;                     // window candidates per workgroup
+#ifndef VGPOSP_WIN_CAND
+#define VGPOSP_WIN_CAND 2  // (A/B builds: 1 / 2 / 3 / 4 / 6 measured)
+#endif
+constexpr int WIN_CAND = VGPOSP_WIN_CAND;       // window candidates per workgroup
 constexpr int WIN_T = 64 * (2 + WIN_CAND);      // threads per workgroup
 
-// The window kernel after its staging barrier: waves 0 and 1 the pick's new rows, 2 .. 5 one
+// The window kernel after its staging barrier: waves 0 and 1 the pick's new rows, the others one
 // window candidate each (R: the rows in LDS or in the workspace).
 template <int KIND, class R>
 __device__ __forceinline__ void window_tail(const EArgs& a, const double* __restrict__ qdiag,
@@ -2175,27 +2178,6 @@ __device__ __forceinline__ void window_tail(const EArgs& a, const double* __rest
   }
 }
 
-template <int KIND>
-__global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
-                                                             double* cache, const unsigned char* sel,
-                                                             ExactWS w, int round,
-                                                             const long long* picks) {
-  __shared__ RowsLds sm;
-  __shared__ StagedPicks sp;
-  const long long at = picks[round];
-  if (at < 0) return;
-  const Window v = window_of(a, at);
-  const int nr = round + 1;
-  stage_picks(a, w, picks, nr, sp);
-  if (nr * (nr + 1) <= ROWS_LDS) {
-    const LRows L = stage_rows(w, round, sm);
-    __syncthreads();
-    window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, L, &sm);
-  } else {
-    __syncthreads();
-    window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, global_rows(w), nullptr);
-  }
-}
 
 // Part 3: refresh the block keys of the window rows (each (j0, j1) row is one contiguous i2 run),
 // then their superblock keys.  The whole workgroup calls it (at >= 0: the window's centre).
@@ -2533,18 +2515,18 @@ __device__ long long block_argmax_lds(const StepLds& L, long long nsb) {
 // the rounds from the stalled one.  One workgroup; a round is this kernel plus the window
 // re-score (exact_window_kernel).  A stalled round refreshed the keys of round - 1's pick first,
 // so the stall / refinement kernels that run next see current keys.
+union StepSm {
+  StepLds k;
+  RowsLds r;
+};
+
+// The step of `round` by one workgroup of SEL_THREADS threads (exact_step_kernel, or the last
+// workgroup of the previous round's window kernel).
 template <int KIND>
-__global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, double* cache,
-                                                                 unsigned char* sel, ExactWS w,
-                                                                 long long nblk, long long nsb,
-                                                                 int nslots, int round, int B,
-                                                                 int rows, long long* picks,
-                                                                 double* pick_delta) {
-  __shared__ int s_slot;
-  __shared__ union {
-    StepLds k;
-    RowsLds r;
-  } sm;
+__device__ __forceinline__ void step_body(const EArgs& ea, double* cache, unsigned char* sel,
+                                          const ExactWS& w, long long nblk, long long nsb,
+                                          int nslots, int round, int rows, long long* picks,
+                                          double* pick_delta, StepSm& sm, int& s_slot) {
   DBG_DECL
   DBG_T(0)
   if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
@@ -2606,6 +2588,41 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, doubl
   // stall: the batch is chosen by exact_stall_kernel, which the host launches first thing in
   // the refinement (vgposp_exact_refine_pending)
   if (threadIdx.x == 0) w.ctl[CTL_STALL] = round;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(SEL_THREADS) void exact_step_kernel(EArgs ea, double* cache,
+                                                                 unsigned char* sel, ExactWS w,
+                                                                 long long nblk, long long nsb,
+                                                                 int nslots, int round, int B,
+                                                                 int rows, long long* picks,
+                                                                 double* pick_delta) {
+  __shared__ int s_slot;
+  __shared__ StepSm sm;
+  (void)B;
+  step_body<KIND>(ea, cache, sel, w, nblk, nsb, nslots, round, rows, picks, pick_delta, sm, s_slot);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(WIN_T) void exact_window_kernel(EArgs a, const double* __restrict__ qdiag,
+                                                             double* cache, const unsigned char* sel,
+                                                             ExactWS w, int round,
+                                                             const long long* picks) {
+  __shared__ RowsLds sm;
+  __shared__ StagedPicks sp;
+  const long long at = picks[round];
+  if (at < 0) return;
+  const Window v = window_of(a, at);
+  const int nr = round + 1;
+  stage_picks(a, w, picks, nr, sp);
+  if (nr * (nr + 1) <= ROWS_LDS) {
+    const LRows L = stage_rows(w, round, sm);
+    __syncthreads();
+    window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, L, &sm);
+  } else {
+    __syncthreads();
+    window_tail<KIND>(a, qdiag, cache, sel, w, round, picks, v, sp, global_rows(w), nullptr);
+  }
 }
 
 // The refinement batch of a stalled round: the B best entries without a column, each given a
