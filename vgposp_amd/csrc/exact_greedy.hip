@@ -45,7 +45,10 @@ constexpr int EB = 256;      // cache entries per block key
 constexpr int ESB = 64;      // blocks per superblock key
 constexpr int CG_BLOCKS = 1024;
 constexpr int CG_T = 256;
-constexpr int CG_SEG = 16;  // lanes per diamond row of the 7-point CG walk (64: one row per wave, slower)
+#ifndef VGPOSP_CG_SEG
+#define VGPOSP_CG_SEG 16
+#endif
+constexpr int CG_SEG = VGPOSP_CG_SEG;  // lanes per diamond row of the 7-point CG walk (64: one row per wave, slower)
 constexpr int CG_RPW = 64 / CG_SEG;  // diamond rows per wave
 constexpr int SEL_THREADS = 1024;
 
@@ -1163,10 +1166,42 @@ __device__ __forceinline__ CGCol cg_col(const ExactWS& w, int j) {
   return c;
 }
 
+// 7-point stencil (the reference's beta = 4 taper): after `it` iterations the Krylov vectors of
+// e_c are supported on the Manhattan ball |d0| + |d1| + |d2| <= it around c, an octahedron of
+// about (4/3) R^3 nodes against the (2R + 1)^3 of the bounding cube (6x fewer at R = 29).  Its
+// nodes are walked row by row: the (d0, d1) rows with |d0| + |d1| <= R (2R^2 + 2R + 1 of them),
+// each a contiguous d2 run of 2 (R - |d0| - |d1|) + 1 nodes, one wave per row.
+__device__ __forceinline__ long long diamond_rows(long long R) { return 2 * R * R + 2 * R + 1; }
+
+// Row `rw` (< diamond_rows(R)) of the diamond, rows ordered by s = |d0| + |d1| (shell s >= 1 has
+// 4 s rows) -> (d0, d1).
+__device__ __forceinline__ void diamond_row(long long rw, long long& d0, long long& d1) {
+  if (rw == 0) {
+    d0 = d1 = 0;
+    return;
+  }
+  // shell s: rows [2 s^2 - 2 s + 1, 2 s^2 + 2 s + 1)
+  long long s = (long long)((sqrt(2.0 * (double)rw - 1.0) + 1.0) * 0.5);
+  while (2 * s * s - 2 * s + 1 > rw) --s;
+  while (2 * (s + 1) * (s + 1) - 2 * (s + 1) + 1 <= rw) ++s;
+  const long long e = rw - (2 * s * s - 2 * s + 1);  // 0 .. 4 s - 1 around the diamond
+  const long long side = e / s, k = e % s;
+  switch (side) {
+    case 0: d0 = s - k; d1 = k; break;        // ( s, 0) -> (0,  s)
+    case 1: d0 = -k; d1 = s - k; break;       // ( 0, s) -> (-s, 0)
+    case 2: d0 = -s + k; d1 = -k; break;      // (-s, 0) -> (0, -s)
+    default: d0 = k; d1 = -s + k; break;      // ( 0,-s) -> ( s, 0)
+  }
+}
+
 // Start the CG solves of S x_j = e_{c_j} (c_j = centers[j], j = blockIdx.y) into column slots
 // slots[j]: r, p0, p1 and the column zeroed except r = e_c, the box [c - H, c + H] per axis
 // shifted inside the grid -> boxlo[slot], rr[0] = 1, state cleared (done when there is no
 // candidate).
+#ifndef VGPOSP_START_DIAMOND
+#define VGPOSP_START_DIAMOND 1  // (A/B builds: 0 clears r, p0, p1 on the whole box)
+#endif
+template <bool OCT>
 __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long long I0, long long I1,
                                                              long long I2, const int* slots,
                                                              const long long* centers) {
@@ -1176,12 +1211,12 @@ __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long lon
   const int slot = slots[j];
   const long long bv = w.b0 * w.b1 * w.b2;
   double* x = w.Qcols + (size_t)slot * bv;
-  long long lc = -1;
+  long long lc = -1, lo0 = 0, lo1 = 0, lo2 = 0;
   if (c >= 0) {
     const long long a0 = c / (I1 * I2), a1 = (c / I2) % I1, a2 = c % I2;
-    const long long lo0 = min(max(a0 - w.H, 0LL), I0 - w.b0);
-    const long long lo1 = min(max(a1 - w.H, 0LL), I1 - w.b1);
-    const long long lo2 = min(max(a2 - w.H, 0LL), I2 - w.b2);
+    lo0 = min(max(a0 - w.H, 0LL), I0 - w.b0);
+    lo1 = min(max(a1 - w.H, 0LL), I1 - w.b1);
+    lo2 = min(max(a2 - w.H, 0LL), I2 - w.b2);
     lc = ((a0 - lo0) * w.b1 + (a1 - lo1)) * w.b2 + (a2 - lo2);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       w.boxlo[3 * slot] = lo0;
@@ -1195,12 +1230,42 @@ __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long lon
     cc.state[1] = 0;
   }
   if (c < 0) return;  // an unused column of the batch: its slot (if any) belongs to someone else
+  if (!OCT || !VGPOSP_START_DIAMOND) {
+    for (long long l = (long long)blockIdx.x * 256 + threadIdx.x; l < bv;
+         l += (long long)gridDim.x * 256) {
+      cc.r[l] = l == lc ? 1.0 : 0.0;
+      cc.p0[l] = 0.0;
+      cc.p1[l] = 0.0;
+      x[l] = 0.0;
+    }
+    return;
+  }
+  // 7-point walk: r, p0 and p1 are read only on the Manhattan ball of radius H + 1 around c (the
+  // walk's nodes, radius <= H, and their face neighbours), so only that ball (inside the box) is
+  // cleared; the column x is read anywhere in the box (qslot_at) and is cleared whole.
   for (long long l = (long long)blockIdx.x * 256 + threadIdx.x; l < bv;
-       l += (long long)gridDim.x * 256) {
-    cc.r[l] = l == lc ? 1.0 : 0.0;
-    cc.p0[l] = 0.0;
-    cc.p1[l] = 0.0;
+       l += (long long)gridDim.x * 256)
     x[l] = 0.0;
+  const long long a0 = c / (I1 * I2), a1 = (c / I2) % I1, a2 = c % I2;
+  const long long R = w.H + 1;
+  const int lane = threadIdx.x & 63, sub = lane / CG_SEG, sl = lane % CG_SEG;
+  const long long nrows = diamond_rows(R);
+  for (long long rw = (((long long)blockIdx.x * 256 + threadIdx.x) >> 6) * CG_RPW + sub; rw < nrows;
+       rw += (((long long)gridDim.x * 256) >> 6) * CG_RPW) {
+    long long d0, d1;
+    diamond_row(rw, d0, d1);
+    const long long j0 = a0 + d0 - lo0, j1 = a1 + d1 - lo1;
+    if (j0 < 0 || j0 >= w.b0 || j1 < 0 || j1 >= w.b1) continue;
+    const long long h = R - (d0 < 0 ? -d0 : d0) - (d1 < 0 ? -d1 : d1);
+    const long long base = (j0 * w.b1 + j1) * w.b2;
+    const long long c2 = a2 - lo2;
+    const long long k0 = max(c2 - h, 0LL), k1 = min(c2 + h, w.b2 - 1);
+    for (long long k = k0 + sl; k <= k1; k += CG_SEG) {
+      const long long l = base + k;
+      cc.r[l] = l == lc ? 1.0 : 0.0;
+      cc.p0[l] = 0.0;
+      cc.p1[l] = 0.0;
+    }
   }
 }
 
@@ -1255,34 +1320,6 @@ __device__ __forceinline__ ActiveCube active_cube(const ExactWS& w, long long I1
   q.e2 = min(a2 + rad, q.lo2 + w.b2 - 1) - q.c2 + 1;
   q.ne = e0 * q.e1 * q.e2;
   return q;
-}
-
-// 7-point stencil (the reference's beta = 4 taper): after `it` iterations the Krylov vectors of
-// e_c are supported on the Manhattan ball |d0| + |d1| + |d2| <= it around c, an octahedron of
-// about (4/3) R^3 nodes against the (2R + 1)^3 of the bounding cube (6x fewer at R = 29).  Its
-// nodes are walked row by row: the (d0, d1) rows with |d0| + |d1| <= R (2R^2 + 2R + 1 of them),
-// each a contiguous d2 run of 2 (R - |d0| - |d1|) + 1 nodes, one wave per row.
-__device__ __forceinline__ long long diamond_rows(long long R) { return 2 * R * R + 2 * R + 1; }
-
-// Row `rw` (< diamond_rows(R)) of the diamond, rows ordered by s = |d0| + |d1| (shell s >= 1 has
-// 4 s rows) -> (d0, d1).
-__device__ __forceinline__ void diamond_row(long long rw, long long& d0, long long& d1) {
-  if (rw == 0) {
-    d0 = d1 = 0;
-    return;
-  }
-  // shell s: rows [2 s^2 - 2 s + 1, 2 s^2 + 2 s + 1)
-  long long s = (long long)((sqrt(2.0 * (double)rw - 1.0) + 1.0) * 0.5);
-  while (2 * s * s - 2 * s + 1 > rw) --s;
-  while (2 * (s + 1) * (s + 1) - 2 * (s + 1) + 1 <= rw) ++s;
-  const long long e = rw - (2 * s * s - 2 * s + 1);  // 0 .. 4 s - 1 around the diamond
-  const long long side = e / s, k = e % s;
-  switch (side) {
-    case 0: d0 = s - k; d1 = k; break;        // ( s, 0) -> (0,  s)
-    case 1: d0 = -k; d1 = s - k; break;       // ( 0, s) -> (-s, 0)
-    case 2: d0 = -s + k; d1 = -k; break;      // (-s, 0) -> (0, -s)
-    default: d0 = k; d1 = -s + k; break;      // ( 0,-s) -> ( s, 0)
-  }
 }
 
 // Visit the active nodes of iteration `it` (grid coordinates): the active cube, thread t its
@@ -1349,6 +1386,58 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   const ActiveCube q = active_cube(w, I1, I2, slots[blockIdx.y], centers[blockIdx.y], it, srad);
   const int m = m1 + 1;
   double acc = 0.0;
+  if constexpr (OCT) {
+    // the 7-point stencil (m1 == 6): the six neighbour offsets in box-index units, and the node's
+    // six neighbours loaded unconditionally — an index outside the box is replaced by the node's
+    // own and its value by 0 — so all twelve loads issue back to back.  Same sum, same order: a
+    // skipped term of the generic walk (coefficient 0 outside the grid, or outside the box) adds
+    // fma(cv, 0 or pj, s) = s here.
+    int od[6][3];
+    long long dl[6];
+#pragma unroll
+    for (int o = 0; o < 6; ++o) {
+      od[o][0] = offs[3 * o];
+      od[o][1] = offs[3 * o + 1];
+      od[o][2] = offs[3 * o + 2];
+      dl[o] = ((long long)od[o][0] * w.b1 + od[o][1]) * w.b2 + od[o][2];
+    }
+    auto node7 = [&](long long g0, long long g1, long long g2) {
+      const long long j0 = g0 - q.lo0, j1 = g1 - q.lo1, j2 = g2 - q.lo2;
+      const long long l = (j0 * w.b1 + j1) * w.b2 + j2;
+      const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * coef_stride(7);
+      double cv[7];
+#pragma unroll
+      for (int o = 0; o < 7; ++o) cv[o] = c[o];
+      double rv[7], pv[7];
+      bool in[7];
+      in[0] = true;
+#pragma unroll
+      for (int o = 0; o < 6; ++o) {
+        const long long k0 = j0 + od[o][0], k1 = j1 + od[o][1], k2 = j2 + od[o][2];
+        in[1 + o] = k0 >= 0 && k0 < w.b0 && k1 >= 0 && k1 < w.b1 && k2 >= 0 && k2 < w.b2;
+      }
+#pragma unroll
+      for (int o = 0; o < 7; ++o) {
+        const long long jj = o == 0 ? l : (in[o] ? l + dl[o - 1] : l);
+        rv[o] = cc.r[jj];
+        pv[o] = it == 0 ? 0.0 : pold[jj];
+      }
+      const double pi = it == 0 ? rv[0] : fma(beta, pv[0], rv[0]);
+      double s = cv[0] * pi;
+#pragma unroll
+      for (int o = 1; o < 7; ++o) {
+        const double pj = it == 0 ? rv[o] : fma(beta, pv[o], rv[o]);
+        s = fma(cv[o], in[o] ? pj : 0.0, s);
+      }
+      pnew[l] = pi;
+      cc.q[l] = s;
+      acc = fma(pi, s, acc);
+    };
+    cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it,
+                 (long long)blockIdx.x * CG_T + threadIdx.x, (long long)gridDim.x * CG_T, node7);
+    block_partial(acc, cc.part_pq, red);
+    return;
+  }
   auto node = [&](long long g0, long long g1, long long g2) {
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
     const double pi = it == 0 ? cc.r[l] : fma(beta, pold[l], cc.r[l]);
@@ -2829,13 +2918,17 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int nb, const int* slots,
   const long long bv = w.b0 * w.b1 * w.b2;
   const int m = a.m1 + 1;
   ProfScope ps("exact_cg", s, 0.0, (double)nb * cg_iters * 8.0 * bv * (m + 9));
-  hipLaunchKernelGGL(exact_cg_start_kernel,
-                     dim3((unsigned)std::min<long long>(ceil_div(bv, 256), 1024), (unsigned)nb),
-                     dim3(256), 0, s, w, a.I0, a.I1, a.I2, slots, centers);
-  VG_LAUNCH_CHECK();
   const double tol2 = cg_tol * cg_tol;
   // the 7-point stencil (face neighbours only): walk the Manhattan ball, not its bounding cube
   const bool oct = a.m1 == 6 && radius == 1;  // (the 6 offsets of squared distance 1)
+  const dim3 sg((unsigned)std::min<long long>(ceil_div(bv, 256), 1024), (unsigned)nb);
+  if (oct)
+    hipLaunchKernelGGL(exact_cg_start_kernel<true>, sg, dim3(256), 0, s, w, a.I0, a.I1, a.I2, slots,
+                       centers);
+  else
+    hipLaunchKernelGGL(exact_cg_start_kernel<false>, sg, dim3(256), 0, s, w, a.I0, a.I1, a.I2, slots,
+                       centers);
+  VG_LAUNCH_CHECK();
   unsigned prev = 1;
   for (int it = 0; it < cg_iters; ++it) {
     // the unclipped active region bounds the launch: a grid that grows with the iterate's support
