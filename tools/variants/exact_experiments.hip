@@ -264,3 +264,154 @@ __global__ __launch_bounds__(BT_T) void exact_bounds_tile_kernel(
 //     (void)nblk, (void)nsb, (void)nslots, (void)pick_delta, (void)s_slot, (void)s_last;
 //   }
 // }
+
+// exact_cg_ab_kernel (round 5): the 7-point CG with one launch per iteration — part B of
+// iteration it - 1 and part A of it together, |r_it|^2 from the recurrence
+// |r - alpha q|^2 = |r|^2 - 2 alpha r.q + alpha^2 q.q (r and q double-buffered by parity, the
+// partials by parity).  WRONG in floating point: the recurrence loses |r|^2 to cancellation once
+// the residual is small, beta goes astray and the solve diverges (GPU: column errors ~1e4 on a
+// 12 x 11 x 10 grid; the same in numpy: plain CG converges in 24 iterations to 7e-16, the
+// recurrence form reaches |r|^2 = 2e9 at the 31-iteration cap).  The stable one-reduction form
+// (Chronopoulos-Gear: r.r and w.r by direct sums, w = A r) moves ~30 % more bytes per iteration
+// and was slower in round 3.  Not built.
+//
+// // The 7-point CG with ONE launch per iteration (A/B build VGPOSP_CG_AB=1).  Launch it does, on the
+// // walk of radius it + 1: part B of iteration it - 1 at every node (x += alpha p_{it-1},
+// // r_it = r_{it-1} - alpha q_{it-1}) and part A of iteration it (p_it = r_it + beta p_{it-1}, formed
+// // on the fly at the neighbours from their r_{it-1}, q_{it-1}, p_{it-1}; q_it = (S + eps I) p_it),
+// // with the partials of p.q, r.q and q.q.  |r_it|^2 comes from the recurrence
+// // |r_{it-1} - alpha q|^2 = |r_{it-1}|^2 - 2 alpha r.q + alpha^2 q.q (no separate |r|^2 pass), so beta
+// // and the stopping test are known at the top of the launch.  r and q alternate between two
+// // buffers by parity (a node's neighbours still read iteration it - 1's values).  last: the closing
+// // launch (it = cg_iters) that applies part B only.  Per element the same fmas as the two-launch
+// // kernels; alpha, beta and the stopping test differ by rounding (the recurrence for |r|^2).
+// __global__ __launch_bounds__(CG_T) void exact_cg_ab_kernel(ExactWS w, long long I0, long long I1,
+//                                                            long long I2, const int* offs,
+//                                                            const int* slots,
+//                                                            const long long* centers, int it,
+//                                                            int np_prev, double tol2, int last) {
+//   __shared__ double red[CG_T / 64];
+//   const CGCol cc = cg_col(w, blockIdx.y);
+//   // converged in an EARLIER launch: state[2 + parity] is written only by block 0 of a launch of
+//   // that parity and read only by the next launch (so no block reads a flag its own launch sets)
+//   const int cur = it & 1, prv = cur ^ 1;
+//   if (centers[blockIdx.y] < 0) return;
+//   if (it > 0 && cc.state[2 + prv]) {
+//     if (blockIdx.x == 0 && threadIdx.x == 0) cc.state[2 + cur] = 1;
+//     return;
+//   }
+//   double alpha = 0.0, beta = 0.0, rr = cc.rr[0];
+//   bool done = last != 0;
+//   if (it > 0) {
+//     // the previous launch's partials (parity it - 1; this launch writes the other set)
+//     const int op = (it - 1) & 1;
+//     const double pq = sum_partials(op ? cc.part_rr : cc.part_pq, np_prev, red);
+//     const double rq = sum_partials(cc.part_rq + op * CG_BLOCKS, np_prev, red);
+//     const double qq = sum_partials(cc.part_qq + op * CG_BLOCKS, np_prev, red);
+//     const double rp = cc.rr[it - 1];
+//     alpha = rp / pq;
+//     rr = fma(alpha, fma(alpha, qq, -2.0 * rq), rp);
+//     beta = rr / rp;
+//     if (blockIdx.x == 0 && threadIdx.x == 0) cc.rr[it] = rr;
+//     if (rr <= tol2) {
+//       done = true;
+//       if (blockIdx.x == 0 && threadIdx.x == 0) {
+//         cc.state[0] = 1;
+//         cc.state[1] = it;
+//         cc.state[2 + cur] = 1;
+//       }
+//     }
+//   }
+//   const int o = prv, nw = cur;
+//   const double* ro = o ? cc.r1 : cc.r;
+//   const double* qo = o ? cc.q1 : cc.q;
+//   const double* po = o ? cc.p1 : cc.p0;
+//   double* rn = nw ? cc.r1 : cc.r;
+//   double* qn = nw ? cc.q1 : cc.q;
+//   double* pn = nw ? cc.p1 : cc.p0;
+//   const int slot = slots[blockIdx.y];
+//   double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
+//   const ActiveCube q = active_cube(w, I1, I2, slot, centers[blockIdx.y], it, 1);
+//   int od[6][3];
+//   long long dl[6];
+// #pragma unroll
+//   for (int k = 0; k < 6; ++k) {
+//     od[k][0] = offs[3 * k];
+//     od[k][1] = offs[3 * k + 1];
+//     od[k][2] = offs[3 * k + 2];
+//     dl[k] = ((long long)od[k][0] * w.b1 + od[k][1]) * w.b2 + od[k][2];
+//   }
+//   double apq = 0.0, arq = 0.0, aqq = 0.0;
+//   auto node = [&](long long g0, long long g1, long long g2) {
+//     const long long j0 = g0 - q.lo0, j1 = g1 - q.lo1, j2 = g2 - q.lo2;
+//     const long long l = (j0 * w.b1 + j1) * w.b2 + j2;
+//     if (it == 0) {  // r_0 = e_c in place, p_0 = r_0
+//       const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * coef_stride(7);
+//       double cv[7], rv[7];
+//       bool in[7];
+//       in[0] = true;
+// #pragma unroll
+//       for (int k = 0; k < 6; ++k) {
+//         const long long k0 = j0 + od[k][0], k1 = j1 + od[k][1], k2 = j2 + od[k][2];
+//         in[1 + k] = k0 >= 0 && k0 < w.b0 && k1 >= 0 && k1 < w.b1 && k2 >= 0 && k2 < w.b2;
+//       }
+// #pragma unroll
+//       for (int k = 0; k < 7; ++k) {
+//         cv[k] = c[k];
+//         rv[k] = cc.r[k == 0 ? l : (in[k] ? l + dl[k - 1] : l)];
+//       }
+//       double sq = cv[0] * rv[0];
+// #pragma unroll
+//       for (int k = 1; k < 7; ++k) sq = fma(cv[k], in[k] ? rv[k] : 0.0, sq);
+//       pn[l] = rv[0];
+//       qn[l] = sq;
+//       apq = fma(rv[0], sq, apq);
+//       arq = fma(rv[0], sq, arq);
+//       aqq = fma(sq, sq, aqq);
+//       return;
+//     }
+//     const double r_own = fma(-alpha, qo[l], ro[l]);
+//     const double p_old = po[l];
+//     x[l] = fma(alpha, p_old, x[l]);
+//     rn[l] = r_own;
+//     if (done) return;
+//     const double* c = w.coef + ((g0 * I1 + g1) * I2 + g2) * coef_stride(7);
+//     double cv[7], rv[7], qv[7], pv[7];
+//     bool in[7];
+//     in[0] = true;
+// #pragma unroll
+//     for (int k = 0; k < 6; ++k) {
+//       const long long k0 = j0 + od[k][0], k1 = j1 + od[k][1], k2 = j2 + od[k][2];
+//       in[1 + k] = k0 >= 0 && k0 < w.b0 && k1 >= 0 && k1 < w.b1 && k2 >= 0 && k2 < w.b2;
+//     }
+// #pragma unroll
+//     for (int k = 0; k < 7; ++k) cv[k] = c[k];
+// #pragma unroll
+//     for (int k = 1; k < 7; ++k) {
+//       const long long jj = in[k] ? l + dl[k - 1] : l;
+//       rv[k] = ro[jj];
+//       qv[k] = qo[jj];
+//       pv[k] = po[jj];
+//     }
+//     const double pi = fma(beta, p_old, r_own);
+//     double sq = cv[0] * pi;
+// #pragma unroll
+//     for (int k = 1; k < 7; ++k) {
+//       const double pj = fma(beta, pv[k], fma(-alpha, qv[k], rv[k]));
+//       sq = fma(cv[k], in[k] ? pj : 0.0, sq);
+//     }
+//     pn[l] = pi;
+//     qn[l] = sq;
+//     apq = fma(pi, sq, apq);
+//     arq = fma(r_own, sq, arq);
+//     aqq = fma(sq, sq, aqq);
+//   };
+//   cg_walk<true>(w, q, I0, I1, I2, centers[blockIdx.y], min(it, last ? it - 1 : it),
+//                 (long long)blockIdx.x * CG_T + threadIdx.x, (long long)gridDim.x * CG_T, node);
+//   if (done) return;
+//   block_partial(apq, nw ? cc.part_rr : cc.part_pq, red);
+//   __syncthreads();  // (red is reused: thread 0 has read it)
+//   block_partial(arq, cc.part_rq + nw * CG_BLOCKS, red);
+//   __syncthreads();
+//   block_partial(aqq, cc.part_qq + nw * CG_BLOCKS, red);
+// }
