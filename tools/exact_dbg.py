@@ -6,6 +6,8 @@ stall: argmax | top-B | slot staging | slot ranking | batch write;
 step: window keys | argmax | slot lookup | pick + key refresh | factor rows;
 --dbg2 (a -DVGPOSP_EXACT_DBG=2 build): the step kernel's key refresh instead — window list |
 level-2 loads | block keys | superblock keys | arg-max;
+--dbg3 (a -DVGPOSP_EXACT_DBG=3 build): the stall kernel's top-B instead — superblock level |
+block level | entry level first pass | entry level merge and output;
 window (workgroup 0, wave 0, which computes the new LQ row; from the end of the staging): - | new
 row | - | wait at the barrier for the candidates' waves | -."""
 import ctypes
@@ -30,7 +32,8 @@ lib = _lib.load()
 buf = (ctypes.c_ulonglong * (64 * 8))()
 lib.vgposp_exact_dbg(buf)  # reset
 out = {}
-for kind, name, phases in ((1, "stall", ["argmax", "topb", "stage", "rank", "write"]),
+for kind, name, phases in ((1, "stall", ["sb_level", "blk_level", "entry_pass1", "entry_merge", "_"] if "--dbg3" in sys.argv
+                            else ["argmax", "topb", "stage", "rank", "write"]),
                            (2, "step", ["list", "loads", "keys", "superkeys", "argmax"] if "--dbg2" in sys.argv
                             else ["window_keys", "argmax", "slot", "pick_keys", "rows"]),
                            (3, "window", ["_", "new_row", "_", "barrier", "_"])):

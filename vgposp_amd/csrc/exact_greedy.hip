@@ -45,10 +45,7 @@ constexpr int EB = 256;      // cache entries per block key
 constexpr int ESB = 64;      // blocks per superblock key
 constexpr int CG_BLOCKS = 1024;
 constexpr int CG_T = 256;
-#ifndef VGPOSP_CG_SEG
-#define VGPOSP_CG_SEG 16
-#endif
-constexpr int CG_SEG = VGPOSP_CG_SEG;  // lanes per diamond row of the 7-point CG walk (64: one row per wave, slower)
+constexpr int CG_SEG = 16;  // lanes per diamond row of the 7-point CG walk (8, 32, 64: slower)
 constexpr int CG_RPW = 64 / CG_SEG;  // diamond rows per wave
 constexpr int SEL_THREADS = 1024;
 
@@ -776,10 +773,7 @@ __device__ __forceinline__ unsigned fast_div(unsigned n, FastDiv f) {
 // Candidates per wave: 2 and 4 measured 0.94-0.96 ms per 128^3 K = 3 pass against 1.41 ms for one
 // (exact_bounds_reg_kernel<1, 6>), 8 spilled to AGPRs at one wave per SIMD (2.1 ms)
 // (profiles/r5_c4_bounds_grouped.jsonl)
-#ifndef VGPOSP_BND_G  // (A/B builds only)
-#define VGPOSP_BND_G 2
-#endif
-constexpr int BND_G = VGPOSP_BND_G;
+constexpr int BND_G = 2;  // candidates per wave (4: no faster, 8: spills)
 template <int G>
 __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
     const double* __restrict__ coef, long long I0, long long I1, long long I2,
@@ -1198,9 +1192,6 @@ __device__ __forceinline__ void diamond_row(long long rw, long long& d0, long lo
 // slots[j]: r, p0, p1 and the column zeroed except r = e_c, the box [c - H, c + H] per axis
 // shifted inside the grid -> boxlo[slot], rr[0] = 1, state cleared (done when there is no
 // candidate).
-#ifndef VGPOSP_START_DIAMOND
-#define VGPOSP_START_DIAMOND 1  // (A/B builds: 0 clears r, p0, p1 on the whole box)
-#endif
 template <bool OCT>
 __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long long I0, long long I1,
                                                              long long I2, const int* slots,
@@ -1230,7 +1221,7 @@ __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long lon
     cc.state[1] = 0;
   }
   if (c < 0) return;  // an unused column of the batch: its slot (if any) belongs to someone else
-  if (!OCT || !VGPOSP_START_DIAMOND) {
+  if (!OCT) {
     for (long long l = (long long)blockIdx.x * 256 + threadIdx.x; l < bv;
          l += (long long)gridDim.x * 256) {
       cc.r[l] = l == lc ? 1.0 : 0.0;
@@ -1564,7 +1555,8 @@ __device__ __forceinline__ void wave_rank_topb(const double* sv, const long long
   int rank[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) rank[q] = 0;
-  for (int j = 0; j < N; ++j) {
+#pragma unroll 16
+  for (int j = 0; j < N; ++j) {  // (unrolled: sixteen broadcast reads in flight, not one)
     const Key o{kv_s[j], ki_s[j]};
 #pragma unroll
     for (int q = 0; q < Q; ++q) rank[q] += key_enc_gt(o, Key{mv[q], mi[q]}) ? 1 : 0;
@@ -1592,16 +1584,29 @@ __device__ __forceinline__ void wave_rank_topb(const double* sv, const long long
 // (<= B), out[1 ..] = their indices, best first.  sv / si: LDS scratch [16 B].  Whole workgroup.
 constexpr int TOPW = 8;  // block_topb_keys' first pass: each wave's best TOPW
 
+// out[0] = the number of leading valid indices among list[0 .. B) (the list ends at the first
+// -1), out[1 ..] = those indices.  One wave, B <= 63.
+__device__ __forceinline__ void topb_out(const long long* list, int B, long long* out) {
+  const int lane = threadIdx.x & 63;
+  const long long k = lane < B ? list[lane] : -1;
+  const int c = __builtin_ctzll(__ballot(lane >= B || k < 0));
+  if (lane < c) out[1 + lane] = k;
+  if (lane == 0) out[0] = c;
+}
+
 template <int P, class KeyFn>
 __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long long* si,
-                               long long* out) {
+                               long long* out, unsigned long long* dt = nullptr) {
   const int t = threadIdx.x, wave = t >> 6;
   constexpr int NW = SEL_THREADS / 64;
   double v[P];
   long long id[P];
-  // items interleaved over the waves (wave w holds items = w mod NW): the best entries of a block
-  // are neighbours in the grid and would otherwise share a wave and force the second pass
-  const int tw = (t & 63) * NW + wave;
+  // items interleaved over the waves by 16-item chunks (chunk c of each SEL_THREADS group to wave
+  // c mod NW, lanes 16 (c / NW) .. + 15): the best entries of a block are grid neighbours and
+  // would otherwise share a wave and force the second pass, while a wave's loads stay four
+  // contiguous 128-byte runs (one item per lane at a stride of NW items had every lane on its own
+  // cache line)
+  const int tw = (((t & 63) >> 4) * NW + wave) * 16 + (t & 15);
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const int i = tw + p * SEL_THREADS;
@@ -1617,6 +1622,7 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
   if (B > TOPW) {
     wave_topb<P>(v, id, TOPW, sv + wave * TOPW, si + wave * TOPW);
     __syncthreads();
+    if (dt != nullptr && t == 0) *dt = __builtin_amdgcn_s_memrealtime();  // (debug builds)
     if (wave == 0) {
       constexpr int Q1 = NW * TOPW / 64;  // items per lane; lanes 4s .. 4s + 3 hold wave s's
       static_assert(Q1 == 2 && TOPW == 8, "merge layout: two items per lane, four lanes per wave");
@@ -1642,15 +1648,7 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
     }
     __syncthreads();
     if (!s_full) {
-      if (wave == 0 && (t & 63) == 0) {
-        int c = 0;
-        for (int b = 0; b < B; ++b) {
-          const long long k = si[NW * CG_B + b];
-          if (k < 0) break;
-          out[1 + c++] = k;
-        }
-        out[0] = c;
-      }
+      if (wave == 0) topb_out(si + NW * CG_B, B, out);
       __syncthreads();
       return (int)out[0];
     }
@@ -1668,15 +1666,10 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
       id2[q] = i < NW * B ? si[i] : -1;
     }
     wave_topb<Q>(v2, id2, B, sv + NW * CG_B, si + NW * CG_B);
-    if ((t & 63) == 0) {
-      int c = 0;
-      for (int b = 0; b < B; ++b) {
-        const long long k = si[NW * CG_B + b];
-        if (k < 0) break;
-        out[1 + c++] = k;
-      }
-      out[0] = c;
-    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    topb_out(si + NW * CG_B, B, out);
   }
   __syncthreads();
   return (int)out[0];
@@ -1688,7 +1681,10 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
 // candidates, best first (out[1] is the arg-max).  The whole workgroup calls it.
 __device__ void block_topb_entries(const double* cache, const unsigned char* sel, long long n,
                                    const ExactWS& w, long long nblk, long long nsb, int B,
-                                   long long* out) {
+                                   long long* out, unsigned long long* dt = nullptr) {
+  // (dt: debug builds with VGPOSP_EXACT_DBG=3 stamp the three levels, dt[1] .. dt[4])
+#define DBG_TB(k) \
+  if (dt != nullptr && threadIdx.x == 0) dt[k] = __builtin_amdgcn_s_memrealtime();
   constexpr int NW = SEL_THREADS / 64;
   __shared__ double sv[NW * CG_B + CG_B];
   __shared__ long long si[NW * CG_B + CG_B];
@@ -1706,19 +1702,25 @@ __device__ void block_topb_entries(const double* cache, const unsigned char* sel
     __syncthreads();
     return;
   }
+  DBG_TB(1)
   // blocks of those superblocks (their keys' candidates name them)
   const int nb = block_topb_keys<2>(ns * ESB, B, [&](int i, double& v, long long& k) {
     const long long b = (sbs[1 + i / ESB] / (EB * ESB)) * ESB + (i % ESB);
     v = b < nblk ? w.bval[b] : 0.0;
     k = b < nblk ? w.bidx[b] : -1;
   }, sv, si, blks);
+  DBG_TB(2)
   // entries of those blocks
   block_topb_keys<8>(nb * EB, B, [&](int i, double& v, long long& k) {
     const long long y = (blks[1 + i / EB] / EB) * EB + (i % EB);
-    const bool ok = y < n && !sel[y];
-    v = ok ? cache[y] : 0.0;
+    const long long yc = y < n ? y : n - 1;  // (both loads issued together, neither behind the other)
+    const double cv = cache[yc];
+    const bool ok = y < n && !sel[yc];
+    v = ok ? cv : 0.0;
     k = ok ? y : -1;
-  }, sv, si, out);
+  }, sv, si, out, dt != nullptr ? dt + 3 : nullptr);
+  DBG_TB(4)
+#undef DBG_TB
 }
 
 __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int nslots) {
@@ -2207,10 +2209,7 @@ __device__ __forceinline__ Window window_of(const EArgs& a, long long at) {
 // own rows (row `round` of LQ and LS: every workgroup, the same values, so the same bits written to
 // the workspace), the others one window candidate each — their right-hand sides and the substitution
 // of rows 0 .. round-1 run WHILE the new rows are computed; after one barrier the last row.
-#ifndef VGPOSP_WIN_CAND
-#define VGPOSP_WIN_CAND 2  // (A/B builds: 1 / 2 / 3 / 4 / 6 measured)
-#endif
-constexpr int WIN_CAND = VGPOSP_WIN_CAND;       // window candidates per workgroup
+constexpr int WIN_CAND = 2;  // window candidates per workgroup (1 / 3 / 4 / 6 / 14: DESIGN.md §4a)
 constexpr int WIN_T = 64 * (2 + WIN_CAND);      // threads per workgroup
 
 // The window kernel after its staging barrier: waves 0 and 1 the pick's new rows, the others one
@@ -2727,13 +2726,22 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
   DBG_T(0)
   if (w.ctl[CTL_STALL] < 0) return;
   const long long a = block_argmax(w, nsb);
+#if VGPOSP_EXACT_DBG != 3
   DBG_T(1)
+#endif
   // stall: the B best entries without a column become the refinement batch.  The slot table is
   // staged in LDS and ranked in parallel (a first version walked it with thread 0's dependent
   // global loads: 750 us per stall at B = 32): free slots are taken first, lowest index first,
   // then the unpinned ones, oldest refinement first — the candidates in the batch have no column,
   // so no slot of theirs can be recycled.
+#if VGPOSP_EXACT_DBG == 3
+  DBG_T(0)
+  block_topb_entries(cache, sel, n, w, nblk, nsb, B, top, dbg_t);
+  DBG_T(5)
+  DBG_END(1)
+#else
   block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
+#endif
   DBG_T(2)
   __shared__ long long s_cand[EX_SLOTS_MAX];
   __shared__ int s_age[EX_SLOTS_MAX], s_inv_free[EX_SLOTS_MAX], s_inv_old[EX_SLOTS_MAX];
@@ -2762,6 +2770,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
   if (t < nslots) {
     const bool fr = s_cand[t] < 0, old = !fr && !s_pin[t];
     int rank = 0;
+#pragma unroll 8
     for (int i = 0; i < nslots; ++i) {
       if (fr) rank += s_cand[i] < 0 && i < t;
       else if (old) rank += s_cand[i] >= 0 && !s_pin[i] && (s_age[i] < s_age[t] || (s_age[i] == s_age[t] && i < t));
@@ -2776,51 +2785,59 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
   }
   __syncthreads();
   DBG_T(4)
-  if (t == 0) {
+  if (t < 64) {
     // without a column: a candidate still on its K_lo bound is tightened (K_hi bound, cheap); one
     // already tightened (or exact but recycled), and the arg-max itself, gets its CG column (the
-    // arg-max would stall the next event on its own otherwise)
-    long long* todo = s_todo;
-    int nt = 0, ntight = 0;
-    for (int b = 0; b < ntop; ++b) {
-      if (s_has[b]) continue;
-      const long long y = top[1 + b];
-      if (s_qx[b] == 0 && y != a) w.rt_cand[ntight++] = y;
-      else todo[nt++] = y;
-    }
-    if (nt == 0 && ntight == 0) {
-      if (s_qx[CG_B] == 0) w.rt_cand[ntight++] = a;
-      else todo[nt++] = a;
-    }
-    w.ctl[CTL_NT] = ntight;
-    const int nfree = s_nfree, nold = s_nold;
-    int nb = 0, age = w.ctl[CTL_AGE], recycled = 0;
-    for (int j = 0; j < nt; ++j) {
-      int slot_j;
-      if (j < nfree) {
-        slot_j = s_inv_free[j];
-      } else if (j - nfree < nold) {
-        slot_j = s_inv_old[j - nfree];
-        ++recycled;  // its candidate loses its column (it is bounded again)
+    // arg-max would stall the next event on its own otherwise).  Wave 0, lane b for top entry b:
+    // the two lists keep the entries' order (prefix counts), slot j goes to the j-th column.
+    const int lane = t;
+    const bool live = lane < ntop && !s_has[lane];
+    const long long y = lane < ntop ? top[1 + lane] : -1;
+    const bool tight = live && s_qx[lane] == 0 && y != a;
+    const bool col = live && !tight;
+    const unsigned long long mt = __ballot(tight), mc = __ballot(col);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int ntight = __popcll(mt), nt = __popcll(mc);
+    if (tight) w.rt_cand[__popcll(mt & below)] = y;
+    if (col) s_todo[__popcll(mc & below)] = y;
+    if (nt == 0 && ntight == 0) {  // (wave-uniform)
+      if (s_qx[CG_B] == 0) {
+        if (lane == 0) w.rt_cand[0] = a;
+        ntight = 1;
       } else {
-        break;
+        if (lane == 0) s_todo[0] = a;
+        nt = 1;
       }
-      w.rl_cand[slot_j] = todo[j];
-      w.rl_age[slot_j] = age++;
-      w.rf_cand[nb] = todo[j];
-      w.rf_slot[nb] = slot_j;
-      ++nb;
     }
-    for (int j = nb; j < CG_B; ++j) {
-      w.rf_cand[j] = -1;
-      w.rf_slot[j] = -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nfree = s_nfree, nold = s_nold;
+    const int nb = min(nt, nfree + nold), recycled = nb - min(nb, nfree);
+    const int age = w.ctl[CTL_AGE];
+    if (lane < nb) {
+      // free slots first; then the unpinned ones (their candidates lose their columns: bounded again)
+      const int slot_j = lane < nfree ? s_inv_free[lane] : s_inv_old[lane - nfree];
+      const long long yj = s_todo[lane];
+      w.rl_cand[slot_j] = yj;
+      w.rl_age[slot_j] = age + lane;
+      w.rf_cand[lane] = yj;
+      w.rf_slot[lane] = slot_j;
+    } else if (lane < CG_B) {
+      w.rf_cand[lane] = -1;
+      w.rf_slot[lane] = -1;
     }
-    w.ctl[CTL_AGE] = age;
-    w.ctl[CTL_UNPICKED] -= recycled;
-    w.ctl[CTL_NB] = nb;
+    if (lane == 0) {
+      w.ctl[CTL_NT] = ntight;
+      w.ctl[CTL_AGE] = age + nb;
+      w.ctl[CTL_UNPICKED] -= recycled;
+      w.ctl[CTL_NB] = nb;
+    }
   }
   DBG_T(5)
+#if VGPOSP_EXACT_DBG != 3
   DBG_END(1)
+#endif
 }
 
 }  // namespace vgposp
