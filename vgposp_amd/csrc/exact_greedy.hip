@@ -877,11 +877,27 @@ __global__ __launch_bounds__(256) void exact_pt_hist_kernel(const double* cache,
   const int shift = pt_shift(pass);
   const unsigned long long prefix = pass == 0 ? 0ull : (unsigned long long)state[0];
   const unsigned long long pmask = pass == 0 ? 0ull : ~((1ull << (shift + 12)) - 1);
-  for (long long y = (long long)blockIdx.x * 256 + threadIdx.x; y < n;
-       y += (long long)gridDim.x * 256) {
-    if (qexact[y] != 0) continue;
-    const unsigned long long c = key_enc(cache[y], y).v;
-    if ((c & pmask) == prefix) atomicAdd(&h[(c >> shift) & (PT_BINS - 1)], 1u);
+  const int lane = threadIdx.x & 63;
+  for (long long y0 = (long long)blockIdx.x * 256; y0 < n; y0 += (long long)gridDim.x * 256) {
+    const long long y = y0 + threadIdx.x;
+    bool act = false;
+    unsigned bin = 0;
+    if (y < n && qexact[y] == 0) {
+      const unsigned long long c = key_enc(cache[y], y).v;
+      act = (c & pmask) == prefix;
+      bin = (unsigned)(c >> shift) & (PT_BINS - 1);
+    }
+    // one LDS atomic per distinct bin of the wave (the first pass puts nearly every code in a few
+    // bins: lane-per-lane atomics on one address serialise)
+    unsigned long long m = __ballot(act);
+    while (m != 0ull) {
+      const int l0 = __builtin_ctzll(m);
+      const unsigned b0 = __shfl(bin, l0, 64);
+      const unsigned long long same = __ballot(act && bin == b0);
+      if (lane == l0) atomicAdd(&h[b0], (unsigned)__popcll(same));
+      if (act && bin == b0) act = false;
+      m &= ~same;
+    }
   }
   __syncthreads();
   for (int b = threadIdx.x; b < PT_BINS; b += 256)
@@ -949,11 +965,22 @@ __global__ __launch_bounds__(256) void exact_pt_list_kernel(const double* cache,
                                                             long long n, long long* state,
                                                             long long* list, int* count) {
   const unsigned long long thr = (unsigned long long)state[0];
-  for (long long y = (long long)blockIdx.x * 256 + threadIdx.x; y < n;
-       y += (long long)gridDim.x * 256) {
-    if (qexact[y] != 0 || key_enc(cache[y], y).v < thr) continue;
-    const unsigned long long i = atomicAdd((unsigned long long*)&state[3], 1ull);
-    if (i < (unsigned long long)PT_MAX) list[i] = y;
+  const int lane = threadIdx.x & 63;
+  for (long long y0 = (long long)blockIdx.x * 256; y0 < n; y0 += (long long)gridDim.x * 256) {
+    const long long y = y0 + threadIdx.x;
+    const bool in = y < n && qexact[y] == 0 && key_enc(cache[y], y).v >= thr;
+    // one atomic per wave (lane-per-lane atomics on one counter serialise); the listed SET does
+    // not depend on the order the waves get their ranges in
+    const unsigned long long m = __ballot(in);
+    if (m == 0ull) continue;
+    unsigned long long base = 0;
+    if (lane == __builtin_ctzll(m))
+      base = atomicAdd((unsigned long long*)&state[3], (unsigned long long)__popcll(m));
+    base = __shfl(base, __builtin_ctzll(m), 64);
+    if (in) {
+      const unsigned long long i = base + __popcll(m & ((1ull << lane) - 1ull));
+      if (i < (unsigned long long)PT_MAX) list[i] = y;
+    }
   }
   (void)count;
 }
@@ -3308,7 +3335,8 @@ extern "C" int vgposp_exact_pretighten(VGPOSP_EXACT_PARAMS, const int* tab_off,
   VG_CHECK_ARG(a.m1 == 6, 12);  // the register bounds kernel (the 7-point taper)
   VG_CHECK_ARG(a.n < (1LL << 31), 3);
   const long long n = a.n, nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
-  const unsigned sweep = (unsigned)std::min<long long>(ceil_div(n, 256), 2048);
+  // (512 workgroups: each merges its 4,096-bin histogram into the global one with atomics)
+  const unsigned sweep = (unsigned)std::min<long long>(ceil_div(n, 256), 512);
   double* out = const_cast<double*>(qdiag);
   ProfScope ps("exact_pretighten", s, 0.0, 0.0);
   VG_HIP(vg_memset(w.pt_hist, 0, 4 * (size_t)PT_BINS, s));
