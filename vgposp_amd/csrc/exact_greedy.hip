@@ -682,18 +682,15 @@ __device__ __forceinline__ double lds_f64(unsigned addr) {
 template <int G>
 __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const unsigned (&nba)[G][6],
                                                 double* pl, const int* cntl, int K, double hi_scale,
-                                                double mu, int l) {
+                                                double mu, int l, int ctr) {
   constexpr int LPC = 64 / G;
   double r[G], p[G], q[G];
 #pragma unroll
   for (int s = 0; s < G; ++s) {
     r[s] = (s == 0 && l == 0) ? 1.0 : 0.0;
     p[s] = r[s];
-    pl[s * LPC + l] = r[s];
+    pl[s * LPC + l] = r[s];  // (read from step 1 on: the slots step 0 leaves as they are)
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // the Gauss-Radau recursion in projective form, gamma^mu = N / D (radau_step without its
   // division: gamma - alpha = (N - alpha D) / D, so N' = N - alpha D, D' = mu N' + delta D), and
   // alpha = rr / pq, delta = beta = rn / rr from ONE reciprocal of pq rr per step: the division
@@ -702,18 +699,32 @@ __device__ __forceinline__ double bounds_cg_grp(const double (&c)[G][7], const u
   for (int it = 0; it < K; ++it) {
     const int cnt = cntl[it + 1];
     double pq = 0.0;
+    if (it == 0) {
+      // p_0 = e_y: q_0 = S e_y is the centre's column, read off the coefficient rows — node 0's
+      // diagonal, and for a neighbour of the centre (ctr = the offset that points back to it) its
+      // coefficient toward it — and p_0 . q_0 is the centre's diagonal.  Bit-identical to the
+      // gather and the group sum: every other term there is fma(c, 0, .) or + 0.
+      double q0 = 0.0;
 #pragma unroll
-    for (int s = 0; s < G; ++s) {
-      q[s] = 0.0;
-      if (s * LPC < cnt) {
-        double acc = c[s][0] * p[s];
+      for (int o = 0; o < 6; ++o) q0 = ctr == o ? c[0][1 + o] : q0;
+      if (l == 0) q0 = c[0][0];
 #pragma unroll
-        for (int o = 0; o < 6; ++o) acc = fma(c[s][1 + o], lds_f64(nba[s][o]), acc);
-        q[s] = s * LPC + l < cnt ? acc : 0.0;
-        pq = fma(p[s], q[s], pq);
+      for (int s = 0; s < G; ++s) q[s] = s == 0 && l < cnt ? q0 : 0.0;
+      pq = __shfl(c[0][0], (threadIdx.x & 63) - l, 64);
+    } else {
+#pragma unroll
+      for (int s = 0; s < G; ++s) {
+        q[s] = 0.0;
+        if (s * LPC < cnt) {
+          double acc = c[s][0] * p[s];
+#pragma unroll
+          for (int o = 0; o < 6; ++o) acc = fma(c[s][1 + o], lds_f64(nba[s][o]), acc);
+          q[s] = s * LPC + l < cnt ? acc : 0.0;
+          pq = fma(p[s], q[s], pq);
+        }
       }
+      pq = group_sum<LPC>(pq);
     }
-    pq = group_sum<LPC>(pq);
     const double inv = 1.0 / (pq * rr);
     const double alpha = rr * rr * inv;
     g = fma(alpha, rr, g);
@@ -801,6 +812,10 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
   const unsigned plb = (unsigned)(size_t)(__attribute__((address_space(3))) void*)pl;
   unsigned nba[G][6];
   int ofr[G];
+  // the offset of node l (slot 0) that points back to node 0, the centre (-1: none)
+  int ctr = -1;
+#pragma unroll
+  for (int o = 0; o < 6; ++o) ctr = (l < T && nbl[l * M1 + o] == 0) ? o : ctr;
 #pragma unroll
   for (int s = 0; s < G; ++s) {
     const int j = s * LPC + l;
@@ -836,7 +851,7 @@ __global__ __launch_bounds__(BND_T) void exact_bounds_grp_kernel(
       }
       load_coef_row<M>(coef, gi, c[s]);
     }
-    const double ub = bounds_cg_grp<G>(c, nba, pl, cntl, K, hi_scale, mu, l);
+    const double ub = bounds_cg_grp<G>(c, nba, pl, cntl, K, hi_scale, mu, l, ctr);
     if (live && l == 0) qhi[y] = ub;
   }
 }
