@@ -2980,7 +2980,8 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int nb, const int* slots,
   const double tol2 = cg_tol * cg_tol;
   // the 7-point stencil (face neighbours only): walk the Manhattan ball, not its bounding cube
   const bool oct = a.m1 == 6 && radius == 1;  // (the 6 offsets of squared distance 1)
-  const dim3 sg((unsigned)std::min<long long>(ceil_div(bv, 256), 1024), (unsigned)nb);
+  // ~8 elements per thread (one per thread had 800 short workgroups per column, 42 us a batch)
+  const dim3 sg((unsigned)std::min<long long>(ceil_div(bv, 256 * 8), 1024), (unsigned)nb);
   if (oct)
     hipLaunchKernelGGL(exact_cg_start_kernel<true>, sg, dim3(256), 0, s, w, a.I0, a.I1, a.I2, slots,
                        centers);
