@@ -1230,6 +1230,28 @@ __device__ __forceinline__ void diamond_row(long long rw, long long& d0, long lo
   }
 }
 
+// A CG launch's 1-D grid over nb columns x nbx blocks.  With nb a multiple of 8 every column's
+// blocks run on ONE XCD (workgroup id mod 8 = the XCD): column j on XCD j mod 8, so the
+// neighbour rows a block gathers — written by the column's other blocks — are in that XCD's L2.
+struct CGBlk {
+  int col, bx, nbx;
+};
+
+__device__ __forceinline__ CGBlk cg_blk(int nb) {
+  CGBlk b;
+  b.nbx = (int)gridDim.x / nb;
+  const int id = (int)blockIdx.x;
+  if ((nb & 7) == 0) {
+    const int x = id & 7, k = id >> 3;
+    b.col = x + 8 * (k / b.nbx);
+    b.bx = k % b.nbx;
+  } else {
+    b.col = id / b.nbx;
+    b.bx = id % b.nbx;
+  }
+  return b;
+}
+
 // Start the CG solves of S x_j = e_{c_j} (c_j = centers[j], j = blockIdx.y) into column slots
 // slots[j]: r, p0, p1 and the column zeroed except r = e_c, the box [c - H, c + H] per axis
 // shifted inside the grid -> boxlo[slot], rr[0] = 1, state cleared (done when there is no
@@ -1302,6 +1324,7 @@ __global__ __launch_bounds__(256) void exact_cg_start_kernel(ExactWS w, long lon
   }
 }
 
+
 // Deterministic block reduction of the first `np` partials (every block computes the same sum).
 __device__ __forceinline__ double sum_partials(const double* part, int np, double* red) {
   const int t = threadIdx.x;
@@ -1317,7 +1340,7 @@ __device__ __forceinline__ double sum_partials(const double* part, int np, doubl
   return tot;
 }
 
-__device__ __forceinline__ void block_partial(double v, double* part, double* red) {
+__device__ __forceinline__ void block_partial(double v, double* part, double* red, int bx) {
   v = wave_sum(v);
   const int t = threadIdx.x;
   if ((t & 63) == 0) red[t >> 6] = v;
@@ -1326,7 +1349,7 @@ __device__ __forceinline__ void block_partial(double v, double* part, double* re
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < CG_T / 64; ++i) s += red[i];
-    part[blockIdx.x] = s;
+    part[bx] = s;
   }
 }
 
@@ -1399,15 +1422,16 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
                                                           long long I2, const int* offs, int m1,
                                                           int srad, const int* slots,
                                                           const long long* centers, int it,
-                                                          int np_prev, double tol2) {
+                                                          int np_prev, double tol2, int nb) {
   __shared__ double red[CG_T / 64];
-  const CGCol cc = cg_col(w, blockIdx.y);
+  const CGBlk bk = cg_blk(nb);
+  const CGCol cc = cg_col(w, bk.col);
   if (cc.state[0]) return;
   // |r_it|^2 from the B kernel's partials (every block sums them in the same order)
   const double rr = it == 0 ? cc.rr[0] : sum_partials(cc.part_rr, np_prev, red);
-  if (it > 0 && blockIdx.x == 0 && threadIdx.x == 0) cc.rr[it] = rr;
+  if (it > 0 && bk.bx == 0 && threadIdx.x == 0) cc.rr[it] = rr;
   if (rr <= tol2) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bk.bx == 0 && threadIdx.x == 0) {
       cc.state[0] = 1;
       cc.state[1] = it;
     }
@@ -1416,7 +1440,7 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
   const double beta = it == 0 ? 0.0 : rr / cc.rr[it - 1];
   const double* pold = (it & 1) ? cc.p0 : cc.p1;  // p_{it-1}
   double* pnew = (it & 1) ? cc.p1 : cc.p0;        // p_it
-  const ActiveCube q = active_cube(w, I1, I2, slots[blockIdx.y], centers[blockIdx.y], it, srad);
+  const ActiveCube q = active_cube(w, I1, I2, slots[bk.col], centers[bk.col], it, srad);
   const int m = m1 + 1;
   double acc = 0.0;
   if constexpr (OCT) {
@@ -1466,9 +1490,9 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
       cc.q[l] = s;
       acc = fma(pi, s, acc);
     };
-    cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it,
-                 (long long)blockIdx.x * CG_T + threadIdx.x, (long long)gridDim.x * CG_T, node7);
-    block_partial(acc, cc.part_pq, red);
+    cg_walk<OCT>(w, q, I0, I1, I2, centers[bk.col], it,
+                 (long long)bk.bx * CG_T + threadIdx.x, (long long)bk.nbx * CG_T, node7);
+    block_partial(acc, cc.part_pq, red, bk.bx);
     return;
   }
   auto node = [&](long long g0, long long g1, long long g2) {
@@ -1490,9 +1514,9 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
     cc.q[l] = s;
     acc = fma(pi, s, acc);
   };
-  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, (long long)blockIdx.x * CG_T + threadIdx.x,
-               (long long)gridDim.x * CG_T, node);
-  block_partial(acc, cc.part_pq, red);
+  cg_walk<OCT>(w, q, I0, I1, I2, centers[bk.col], it, (long long)bk.bx * CG_T + threadIdx.x,
+               (long long)bk.nbx * CG_T, node);
+  block_partial(acc, cc.part_pq, red, bk.bx);
 }
 
 // CG iteration it, part B: alpha = |r|^2 / p.q, x += alpha p, r -= alpha q, partials of |r|^2
@@ -1500,16 +1524,18 @@ __global__ __launch_bounds__(CG_T) void exact_cg_a_kernel(ExactWS w, long long I
 template <bool OCT>
 __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I0, long long I1,
                                                           long long I2, int srad, const int* slots,
-                                                          const long long* centers, int it) {
+                                                          const long long* centers, int it,
+                                                          int nb) {
   __shared__ double red[CG_T / 64];
-  const CGCol cc = cg_col(w, blockIdx.y);
+  const CGBlk bk = cg_blk(nb);
+  const CGCol cc = cg_col(w, bk.col);
   if (cc.state[0]) return;
-  const double pq = sum_partials(cc.part_pq, (int)gridDim.x, red);  // the A kernel's grid
+  const double pq = sum_partials(cc.part_pq, bk.nbx, red);  // the A kernel's grid
   const double alpha = cc.rr[it] / pq;
   const double* p = (it & 1) ? cc.p1 : cc.p0;
-  const int slot = slots[blockIdx.y];
+  const int slot = slots[bk.col];
   double* x = w.Qcols + (size_t)slot * (w.b0 * w.b1 * w.b2);
-  const ActiveCube q = active_cube(w, I1, I2, slot, centers[blockIdx.y], it, srad);
+  const ActiveCube q = active_cube(w, I1, I2, slot, centers[bk.col], it, srad);
   double acc = 0.0;
   auto node = [&](long long g0, long long g1, long long g2) {
     const long long l = ((g0 - q.lo0) * w.b1 + (g1 - q.lo1)) * w.b2 + (g2 - q.lo2);
@@ -1518,9 +1544,9 @@ __global__ __launch_bounds__(CG_T) void exact_cg_b_kernel(ExactWS w, long long I
     cc.r[l] = ri;
     acc = fma(ri, ri, acc);
   };
-  cg_walk<OCT>(w, q, I0, I1, I2, centers[blockIdx.y], it, (long long)blockIdx.x * CG_T + threadIdx.x,
-               (long long)gridDim.x * CG_T, node);
-  block_partial(acc, cc.part_rr, red);
+  cg_walk<OCT>(w, q, I0, I1, I2, centers[bk.col], it, (long long)bk.bx * CG_T + threadIdx.x,
+               (long long)bk.nbx * CG_T, node);
+  block_partial(acc, cc.part_rr, red, bk.bx);
 }
 
 // Top-B selection in one workgroup (the refinement batch of a stalled round).  Keys order by
@@ -2998,19 +3024,19 @@ int exact_cg_run(const EArgs& a, const ExactWS& w, int nb, const int* slots,
         CG_BLOCKS, oct ? ceil_div(2 * R * R + 2 * R + 1, (long long)(CG_T / 64 * CG_RPW))
                        : ceil_div(side * side * side, (long long)CG_T));
     if (oct) {
-      hipLaunchKernelGGL(exact_cg_a_kernel<true>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
+      hipLaunchKernelGGL(exact_cg_a_kernel<true>, dim3(blocks * (unsigned)nb), dim3(CG_T), 0, s, w,
                          a.I0, a.I1, a.I2, a.offs, a.m1, radius, slots, centers, it, (int)prev,
-                         tol2);
+                         tol2, nb);
       VG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(exact_cg_b_kernel<true>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
-                         a.I0, a.I1, a.I2, radius, slots, centers, it);
+      hipLaunchKernelGGL(exact_cg_b_kernel<true>, dim3(blocks * (unsigned)nb), dim3(CG_T), 0, s, w,
+                         a.I0, a.I1, a.I2, radius, slots, centers, it, nb);
     } else {
-      hipLaunchKernelGGL(exact_cg_a_kernel<false>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
+      hipLaunchKernelGGL(exact_cg_a_kernel<false>, dim3(blocks * (unsigned)nb), dim3(CG_T), 0, s, w,
                          a.I0, a.I1, a.I2, a.offs, a.m1, radius, slots, centers, it, (int)prev,
-                         tol2);
+                         tol2, nb);
       VG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(exact_cg_b_kernel<false>, dim3(blocks, (unsigned)nb), dim3(CG_T), 0, s, w,
-                         a.I0, a.I1, a.I2, radius, slots, centers, it);
+      hipLaunchKernelGGL(exact_cg_b_kernel<false>, dim3(blocks * (unsigned)nb), dim3(CG_T), 0, s, w,
+                         a.I0, a.I1, a.I2, radius, slots, centers, it, nb);
     }
     VG_LAUNCH_CHECK();
     prev = blocks;
