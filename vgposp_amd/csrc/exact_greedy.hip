@@ -210,8 +210,10 @@ __device__ __forceinline__ double sigma_diag(const EArgs& a) {
 // Tapered covariance entry S(i, j) for i != j (0 outside the support).
 template <int KIND>
 __device__ __forceinline__ double sigma_off(const EArgs& a, long long i, long long j) {
-  const long long i0 = i / (a.I1 * a.I2), i1 = (i / a.I2) % a.I1, i2 = i % a.I2;
-  const long long j0 = j / (a.I1 * a.I2), j1 = (j / a.I2) % a.I1, j2 = j % a.I2;
+  // (32-bit coordinates: the exact path requires n < 2^31, vgposp_exact_prepare / _coef)
+  const int I1 = (int)a.I1, I2 = (int)a.I2, I12 = I1 * I2, ii = (int)i, jj = (int)j;
+  const int i0 = ii / I12, i1 = (ii - i0 * I12) / I2, i2 = ii - (ii / I2) * I2;
+  const int j0 = jj / I12, j1 = (jj - j0 * I12) / I2, j2 = jj - (jj / I2) * I2;
   const long long e0 = i0 - j0, e1 = i1 - j1, e2 = i2 - j2;
   const long long d2i = e0 * e0 + e1 * e1 + e2 * e2;
   if (d2i >= a.ntau) return 0.0;
@@ -227,7 +229,9 @@ __device__ __forceinline__ double sigma_off(const EArgs& a, long long i, long lo
 __device__ __forceinline__ double qslot_at(const ExactWS& w, int slot, long long y, long long I1,
                                            long long I2) {
   const long long* lo = w.boxlo + 3 * slot;
-  const long long l0 = y / (I1 * I2) - lo[0], l1 = (y / I2) % I1 - lo[1], l2 = y % I2 - lo[2];
+  const int yi = (int)y, i12 = (int)(I1 * I2), i2s = (int)I2;  // (n < 2^31 on this path)
+  const int y0 = yi / i12, y1 = (yi - y0 * i12) / i2s, y2 = yi - (yi / i2s) * i2s;
+  const long long l0 = y0 - lo[0], l1 = y1 - lo[1], l2 = y2 - lo[2];
   if (l0 < 0 || l0 >= w.b0 || l1 < 0 || l1 >= w.b1 || l2 < 0 || l2 >= w.b2) return 0.0;
   return w.Qcols[(size_t)slot * (w.b0 * w.b1 * w.b2) + (l0 * w.b1 + l1) * w.b2 + l2];
 }
@@ -260,13 +264,23 @@ __device__ __forceinline__ void coef_row(const EArgs& a, long long i, double* c)
   const int m = a.m1 + 1;
   c[0] = sigma_diag<KIND>(a) + a.jitter;
   if (coef_stride(m) > m) c[m] = 0.0;
-  const long long i0 = i / (a.I1 * a.I2), i1 = (i / a.I2) % a.I1, i2 = i % a.I2;
+  // grid coordinates by 32-bit division (n < 2^31 on this path), and sigma_off's squared index
+  // distance straight from the offset: sigma_off recomputed both nodes' coordinates with 64-bit
+  // divisions (software sequences) for each of the m1 neighbours.  The same values.
+  const int I1 = (int)a.I1, I2 = (int)a.I2, ii = (int)i;
+  const int i0 = ii / (I1 * I2), ir = ii - i0 * (I1 * I2), i1 = ir / I2, i2 = ir - i1 * I2;
   for (int o = 0; o < a.m1; ++o) {
     const int o0 = a.offs[3 * o], o1 = a.offs[3 * o + 1], o2 = a.offs[3 * o + 2];
-    const long long j0 = i0 + o0, j1 = i1 + o1, j2 = i2 + o2;
+    const int j0 = i0 + o0, j1 = i1 + o1, j2 = i2 + o2;
     double v = 0.0;
-    if (j0 >= 0 && j0 < a.I0 && j1 >= 0 && j1 < a.I1 && j2 >= 0 && j2 < a.I2)
-      v = sigma_off<KIND>(a, i, (j0 * a.I1 + j1) * a.I2 + j2);
+    const int d2i = o0 * o0 + o1 * o1 + o2 * o2;
+    if (j0 >= 0 && j0 < a.I0 && j1 >= 0 && j1 < I1 && j2 >= 0 && j2 < I2 && d2i < a.ntau &&
+        a.tau[d2i] != 0.0) {
+      const long long j = ((long long)j0 * I1 + j1) * I2 + j2;
+      const double d0 = a.X[3 * i] - a.X[3 * j], d1 = a.X[3 * i + 1] - a.X[3 * j + 1],
+                   d2 = a.X[3 * i + 2] - a.X[3 * j + 2];
+      v = a.tau[d2i] * kfun<KIND>(d0 * d0 + d1 * d1 + d2 * d2, a.tla, a.inv_ls, a.inv_ls2);
+    }
     c[1 + o] = v;
   }
 }
@@ -2917,7 +2931,7 @@ namespace {
 #define VGPOSP_EXACT_CHECK_COMMON()                                                          \
   VG_CHECK_ARG(kind >= VGPOSP_KERNEL_EQ && kind <= VGPOSP_KERNEL_MATERN52, 1);             \
   VG_CHECK_ARG(X != nullptr, 2);                                                          \
-  VG_CHECK_ARG(I0 >= 1 && I1 >= 1 && I2 >= 1, 3);                                         \
+  VG_CHECK_ARG(I0 >= 1 && I1 >= 1 && I2 >= 1 && I0 * I1 * I2 < (1LL << 31), 3);           \
   VG_CHECK_ARG(amp > 0.0, 6);                                                             \
   VG_CHECK_ARG(ls > 0.0, 7);                                                              \
   VG_CHECK_ARG(m >= 1 && (m == 1 || offsets != nullptr), 12);                             \
@@ -2971,6 +2985,7 @@ int exact_prepare_t(const EArgs& a, const double* qdiag, double* cache, unsigned
   const long long n = a.n;
   const long long nblk = ceil_div(n, EB), nsb = ceil_div(nblk, ESB);
   const bool bounded = (flags & 1) != 0;
+  VG_CHECK_ARG(n < (1LL << 31), 3);  // (coef_row's 32-bit grid coordinates)
   VG_HIP(vg_memset(sel, 0, n, s));
   VG_HIP(vg_memset(w.lastA, 0, n, s));
   // 0: on the K_lo bound, to be tightened first (flags & 2: a second bound level); 2: final bound
@@ -3158,6 +3173,7 @@ extern "C" int vgposp_exact_round(VGPOSP_EXACT_PARAMS, int round, int last, int6
 extern "C" int vgposp_exact_coef(VGPOSP_EXACT_PARAMS, void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_coef");
   const long long n = a.n;
+  VG_CHECK_ARG(n < (1LL << 31), 3);  // (coef_row's 32-bit grid coordinates)
   const int rc = dispatch_kind(kind, [&](auto K) {
     if (coef_stride(m) == 8)
       hipLaunchKernelGGL(exact_coef8_kernel<decltype(K)::value>, dim3((unsigned)ceil_div(n, 256)),
