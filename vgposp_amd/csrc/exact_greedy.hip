@@ -2506,11 +2506,8 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
   if (dt != nullptr && threadIdx.x == 0) dt[k] = __builtin_amdgcn_s_memrealtime();
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, nwave = blockDim.x >> 6;
   if (nsb > SK_MAXNSB) return false;
-  // level 1: the grid's superblock keys; the distinct blocks / superblocks of the window (wave 0)
-  for (long long q = t; q < nsb; q += blockDim.x) {
-    L.sval[q] = w.sval[q];
-    L.sidx[q] = w.sidx[q];
-  }
+  // level 1: the distinct blocks / superblocks of the window (wave 0, ALU and LDS only); the
+  // grid's superblock keys after it (their loads would stall wave 0's list behind them)
   if (wave == 0) {
     const Window v = window_of(a, at);
     const long long nrow = v.w0 * v.w1;
@@ -2572,17 +2569,17 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
       L.ok = ok && ns <= SK_MAXSB;
     }
   }
+  for (long long q = t; q < nsb; q += blockDim.x) {
+    L.sval[q] = w.sval[q];
+    L.sidx[q] = w.sidx[q];
+  }
   __syncthreads();
   DBG_PT(1)
   if (!L.ok) return false;
   const int nb = L.nb, ns = L.ns;
-  // level 2: the touched superblocks' block keys into LDS, the window blocks' entries (registers)
-  for (int e = t; e < ns * ESB; e += blockDim.x) {
-    const int q = e / ESB, j = e % ESB;
-    const long long b = L.sb[q] * ESB + j;
-    L.bval[q][j] = b < nblk ? w.bval[b] : 0.0;
-    L.bidx[q][j] = b < nblk ? w.bidx[b] : -1;
-  }
+  // level 2: the window blocks' entries (registers) — issued first, so that their round trip
+  // overlaps the one of the touched superblocks' block keys, which go through LDS (the stores wait
+  // on their loads)
   constexpr int PER = EB / 64;
   double c[4][PER];
   unsigned char sl[4][PER];
@@ -2598,9 +2595,18 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const long long y = mine[q] >= 0 ? mine[q] * EB + e * 64 + lane : a.n;
-      c[q][e] = y < a.n ? cache[y] : 0.0;
-      sl[q][e] = y < a.n ? sel[y] : 1;
+      const long long yc = y < a.n ? y : a.n - 1;  // (unconditional loads, masked values)
+      const double cv = cache[yc];
+      const unsigned char sv = sel[yc];
+      c[q][e] = y < a.n ? cv : 0.0;
+      sl[q][e] = y < a.n ? sv : 1;
     }
+  }
+  for (int e = t; e < ns * ESB; e += blockDim.x) {
+    const int q = e / ESB, j = e % ESB;
+    const long long b = L.sb[q] * ESB + j;
+    L.bval[q][j] = b < nblk ? w.bval[b] : 0.0;
+    L.bidx[q][j] = b < nblk ? w.bidx[b] : -1;
   }
   __syncthreads();  // the LDS block keys are in place before the new ones overwrite them
   DBG_PT(2)
