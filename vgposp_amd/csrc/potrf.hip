@@ -52,6 +52,15 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 // Phase stamps for tools/diag_probe.hip (debug builds only; compiled out otherwise).
 #ifdef VGPOSP_STAMPS
 __device__ long long g_stamps[16];
+}  // namespace vgposp
+// (debug builds: the accumulated phase cycles, then cleared; tools/leaf_probe.py)
+extern "C" int vgposp_potrf_stamps(long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgposp::g_stamps), sizeof(long long) * 16) != hipSuccess)
+    return 1;
+  long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(vgposp::g_stamps), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+namespace vgposp {
 #define STAMP_NOW() ((long long)__builtin_amdgcn_s_memtime())
 #define STAMP_ADD(i, t0) \
   if (threadIdx.x == 0) g_stamps[i] += STAMP_NOW() - (t0)
@@ -104,7 +113,8 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 // (Measured alternative: 64-bit DPP row_newbcast folded into v_fmac_f64 is ~12x slower on gfx950.)
 template <bool TALL>
 __device__ __forceinline__ void leaf_panel(double (&D0)[LW], double (&D1)[LW], int lane, int c0,
-                                           int jb, int64_t col0, int* info, double* rdiag) {
+                                           int jb, int64_t col0, int* info, double* rdiag,
+                                           double* pcol) {
   double my_d = 1.0, my_inv = 1.0;  // lane c < 16 keeps column c's pivot and its reciprocal
 #pragma unroll
   for (int c = 0; c < LW; ++c) {
@@ -116,11 +126,18 @@ __device__ __forceinline__ void leaf_panel(double (&D0)[LW], double (&D1)[LW], i
     }
     D0[c] = lane == c ? piv : D0[c] * inv;
     if (TALL) D1[c] *= inv;
+    // L[c0 + k][c0 + c] for k > c, the scaled column on lanes k: through the wave's LDS slot (one
+    // store, then broadcast reads issued together) instead of a v_readlane pair per k
+    if (c + 1 < LW) {
+      if (lane < LW) pcol[lane] = D0[c];
+      wave_sync();
 #pragma unroll
-    for (int k = c + 1; k < LW; ++k) {
-      const double lkc = readlane_d(D0[c], k);  // L[c0 + k][c0 + c]
-      D0[k] -= D0[c] * lkc;
-      if (TALL) D1[k] -= D1[c] * lkc;
+      for (int k = c + 1; k < LW; ++k) {
+        const double lkc = pcol[k];
+        D0[k] -= D0[c] * lkc;
+        if (TALL) D1[k] -= D1[c] * lkc;
+      }
+      wave_sync();  // (the next column's store waits for these reads)
     }
   }
   // statuses and reciprocals once per panel (no branches inside the column steps)
@@ -140,6 +157,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   extern __shared__ double L[];  // [NB][LP2]
   __shared__ double rdiag[NB];
   __shared__ double XD[(NB / LW) * LW * LW];  // dense diagonal blocks of L^-1
+  __shared__ double pcol[LW];                  // wave 0's panel column broadcast (leaf_panel)
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   // invert: 0 = factor (lower(A) <- L), 1 = factor and invert (lower(A) <- L^-1), 2 = A already
@@ -210,8 +228,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
         D0[k] = r0 < JP ? L[r0 * LP2 + c0 + k] : 0.0;
         D1[k] = (tall && r1 < JP) ? L[r1 * LP2 + c0 + k] : 0.0;
       }
-      if (tall) leaf_panel<true>(D0, D1, lane, c0, jb, col0, info, rdiag);
-      else leaf_panel<false>(D0, D1, lane, c0, jb, col0, info, rdiag);
+      if (tall) leaf_panel<true>(D0, D1, lane, c0, jb, col0, info, rdiag, pcol);
+      else leaf_panel<false>(D0, D1, lane, c0, jb, col0, info, rdiag, pcol);
 #pragma unroll
       for (int k = 0; k < LW; ++k) {
         if (r0 < JP && (lane >= LW || k <= lane)) L[r0 * LP2 + c0 + k] = D0[k];
