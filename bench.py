@@ -53,8 +53,8 @@ def parse():
     p.add_argument("--no-vgp", action="store_true", help="skip the C3 / C5 VGP training lines")
     p.add_argument("--no-c2", action="store_true", help="skip the C2 assembly + potrf line")
     p.add_argument("--vgp-steps", type=int, default=10)
-    p.add_argument("--vgp-mixed", action="store_true",
-                   help="also time C5 with the fp32 factor + fp64 refinement (slower than fp64 at "
+    p.add_argument("--no-vgp-mixed", action="store_true",
+                   help="skip C5 as named (the fp32 factor + fp64 refinement; slower than fp64 at "
                         "M = 1,024 on MI355X, DESIGN.md §8)")
     p.add_argument("--no-c4", action="store_true", help="skip the C4 (128^3 exact algorithm 3) line")
     p.add_argument("--c4-steps", type=int, default=10)
@@ -142,6 +142,20 @@ def cpu_baseline(args, N):
     del S
     th_main = max(runs)
     t_inc = runs[th_main]
+    # a second, smaller sample at the same thread count, for a two-point a n^3 + b n^2 model of
+    # the time (the O(n^3) init and the O(n^2) rounds) extrapolated to the headline's N
+    shape_s = (16, 16, 16)
+    S = sigma(shape_s)
+    if threadpool_limits is not None:
+        with threadpool_limits(limits=th_main, user_api="blas"):
+            t0 = time.perf_counter()
+            op.placement_lazy_incremental(S, args.k)
+            t_small = time.perf_counter() - t0
+    else:
+        t0 = time.perf_counter()
+        op.placement_lazy_incremental(S, args.k)
+        t_small = time.perf_counter() - t0
+    del S
     ps = tuple(args.cpu_shape)
     Sp = sigma(ps)
     trace = []
@@ -159,6 +173,12 @@ def cpu_baseline(args, N):
     np.linalg.cholesky(Sc)
     tc = time.perf_counter() - t0
     n_inc = int(np.prod(shape))
+    n_s = int(np.prod(shape_s))
+    # t(n) = a n^3 + b n^2 through (n_s, t_small) and (n_inc, t_inc)
+    den = n_inc ** 3 * n_s ** 2 - n_s ** 3 * n_inc ** 2
+    a3 = (t_inc * n_s ** 2 - t_small * n_inc ** 2) / den
+    b2 = (t_small * n_inc ** 3 - t_inc * n_s ** 3) / den
+    t_fit = a3 * N ** 3 + b2 * N ** 2
     return {
         "value": args.k / t_inc,
         "unit": "placements/s",
@@ -172,13 +192,18 @@ def cpu_baseline(args, N):
                    f"{t_inc:.1f} s; the GPU line is at N={N}, where the O(N^3) init alone is "
                    f"{(N / n_inc) ** 3:.0f}x this sample's"),
         "gpu_same_sample": gpu_same,
-        # the headline's own config is N = 65,536, where the sample's dominant O(N^3) Cholesky +
-        # inverse grows by (N / n)^3 (the O(N^2) rounds by (N / n)^2): the sample's rate divided
-        # by that factor bounds the CPU's rate at the config from ABOVE (timing it there would take
-        # an hour of host time)
-        "at_config_upper_bound": {
+        # the headline's own config is N = 65,536 (timing it there takes most of an hour of host
+        # time: tests/golden/make_golden_65k.py).  Scaling the WHOLE sample time by (N / n)^3
+        # over-scales its O(n^2) rounds and fixed costs, and BLAS runs faster at large n, so that
+        # time is too long and its rate a LOWER bound of the CPU's rate at the config; the
+        # two-point fit a n^3 + b n^2 (samples n = 4,096 and 8,192) is the estimate
+        "at_config_lower_bound": {
             "value": args.k / (t_inc * (N / n_inc) ** 3), "unit": "placements/s", "N": N,
-            "model": f"sample time x (N / {n_inc})^3"},
+            "model": f"whole sample time x (N / {n_inc})^3 (a lower bound of the rate)"},
+        "at_config_estimate": {
+            "value": args.k / t_fit if t_fit > 0 else None, "unit": "placements/s", "N": N,
+            "model": (f"t(n) = a n^3 + b n^2 through n = {n_s} ({t_small:.2f} s) and n = {n_inc} "
+                      f"({t_inc:.2f} s): a = {a3:.3e}, b = {b2:.3e}, t({N}) = {t_fit:.0f} s")},
         "reference_algorithm": {
             "value": args.cpu_k / t_pinv, "unit": "placements/s",
             "sample": (f"pinv restatement of placement_algorithm2.placement_algorithm_2 on a "
@@ -241,8 +266,9 @@ def load_traffic(path, kernel, N, shape, k):
 
 
 def _committed(name, picks):
-    """Whether `picks` equal the selection committed in tests/golden/<name> (written from a
-    one-GPU run; at N > 1 the sharded path must reproduce it), None if absent."""
+    """Whether `picks` equal the selection committed in tests/golden/<name> (the headline's:
+    a CPU run of the same workload; C4's: the C oracle's; at N > 1 the sharded path must
+    reproduce it), None if absent."""
     try:
         with open(os.path.join(ROOT, "tests", "golden", name)) as f:
             want = json.load(f).get("picks")
@@ -301,6 +327,23 @@ def vgp_line(args, which="c3", precision="fp64", world=1, rank=0, barrier=None, 
             ("fp64" if precision == "fp64" else
              f"M x M Cholesky in fp32 (f32 MFMA) + {precision.partition(':')[2] or 3} fp64 "
              "refinement steps (ELBO within 1e-5 of fp64), the rest fp64"))
+    # roofline of the step's dominant kernel, the fp64 MFMA GEMM: its launches' algorithmic flops
+    # (the library's counters: 2 m n k per launch, triangles at their true flops) over their summed
+    # HIP-event time.  Beside it the step's own algorithmic flops over the whole step time:
+    # 2 M^2 N (the products over all N observations) + 2 M^2 B (the minibatch products) + M^3 / 3
+    # (one M x M Cholesky)
+    alg = 2.0 * M * M * N + 2.0 * M * M * B + M ** 3 / 3.0
+    roof = None
+    if ms:
+        ach = fl / (ms * 1e-3) / 1e12
+        roof = {"kernel": "gemm_f64", "bound": "mfma", "unit": "TFLOP/s", "achieved": ach,
+                "peak": FP64_MFMA_PEAK_TFLOPS, "frac": ach / FP64_MFMA_PEAK_TFLOPS,
+                "launches_per_step": n, "avg_launch_ms": ms / max(n, 1),
+                "share_of_step": ms / (dt * 1e3), "traffic": None,
+                "step_algorithmic_flops": alg,
+                "step_algorithmic_tflops": alg / dt / 1e12,
+                "step_frac": alg / dt / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                "measured": "HIP events around every GEMM launch of one eager step (rank 0)"}
     out = {"metric": "VGP ELBO Adam steps/sec", "value": 1.0 / dt, "ms_per_step": dt * 1e3,
            "n_gpus": world, "scaling": "strong" if world > 1 else None,
            "config": {"workload": desc + (", EQ" if kernel == "eq" else ", MaternFiveHalves") +
@@ -311,7 +354,8 @@ def vgp_line(args, which="c3", precision="fp64", world=1, rank=0, barrier=None, 
            "loss_first": first, "loss_last": float(last),
            "graph": bool(train_op.graph),
            "gemm": {"ms_per_step": ms, "tflops": fl / (ms * 1e-3) / 1e12 if ms else None,
-                    "launches_per_step": n, "note": "one eager step with event timing (rank 0)"}}
+                    "launches_per_step": n, "note": "one eager step with event timing (rank 0)"},
+           "roofline": roof}
     if world > 1:
         out["allreduce_doubles_per_step"] = M * M + M + 2 + M * X.shape[1]
     return out
@@ -897,7 +941,7 @@ def main():
     if not args.no_vgp:
         kw = dict(world=world, rank=rank, barrier=barrier, maxtime=maxtime)
         vgp = {"vgp_c3": vgp_line(args, "c3", **kw), "vgp_c5": vgp_line(args, "c5", **kw)}
-        if args.vgp_mixed:  # (retired from the default line: DESIGN.md §8 item 3)
+        if not args.no_vgp_mixed:  # BASELINE configs[4] as named: the fp32 mixed-precision factor
             vgp["vgp_c5_mixed"] = vgp_line(args, "c5", precision="mixed:2", **kw)
     splits = splits_line(args, world, barrier, maxtime, rank) if world > 1 and not args.no_splits \
         else None
@@ -992,7 +1036,9 @@ def main():
         "deterministic_selection": deterministic,
         "selected_head": sel[:8],
         "selected": sel,
-        "matches_committed_picks": (_committed("bench65k_picks.json", sel)
+        # the CPU run of this exact workload (tests/golden/make_golden_65k.py: host LAPACK + the
+        # oracle's incremental lazy greedy at N = 65,536), not a GPU self-pin
+        "matches_committed_picks": (_committed("bench65k_cpu_picks.json", sel)
                                     if (shape == (64, 32, 32) and k == 50 and args.kernel == "eq"
                                         and args.noise == 1e-2) else None),
     }

@@ -258,9 +258,25 @@ def placement_lazy_incremental(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, 
         raise np.linalg.LinAlgError(f"dpotri info {info}")
     del c, Mj
     Q = np.tril(Q) + np.tril(Q, -1).T
-    diag = np.diag(cov).copy()
+    return placement_lazy_columns(np.diag(cov).copy(), lambda y: cov[y], np.diag(Q).copy(),
+                                  lambda y: Q[y], k, lazy=lazy, jitter=jitter, thr=thr,
+                                  cache_init=cache_init, deltas_out=deltas_out)
+
+
+def placement_lazy_columns(sigma_diag, sigma_row, q_diag, q_col, k, lazy=True, jitter=0.0,
+                           thr=DELTA_EPS, cache_init=np.inf, deltas_out=None, margins_out=None,
+                           log=None):
+    """The rounds of placement_lazy_incremental from callbacks, so a caller can hold Sigma and
+    Q = (Sigma + eps I)^-1 however it likes (tests/golden/make_golden_65k.py keeps only the
+    in-place dpotri buffer of N = 65,536 and rebuilds Sigma's rows from the points):
+    ``sigma_diag`` [N], ``sigma_row(y)`` -> Sigma e_y, ``q_diag`` [N] = diag(Q),
+    ``q_col(y)`` -> Q e_y.  Same arithmetic, same decisions (placement_algorithm2.py:151-219).
+    ``margins_out`` receives each round's margin: the pick's value minus the best other
+    non-selected entry it was chosen over (the cache when lazy, the fresh deltas otherwise)."""
+    N = len(sigma_diag)
+    diag = np.asarray(sigma_diag, dtype=np.float64)
     nom = diag.copy()
-    prec = np.diag(Q).copy()
+    prec = np.asarray(q_diag, dtype=np.float64).copy()
     W = np.zeros((k, N))
     V = np.zeros((k, N))
     cache = np.full(N, float(cache_init))
@@ -279,12 +295,19 @@ def placement_lazy_incremental(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, 
             y = int(np.argmax(d))
         if deltas_out is not None:
             deltas_out.append(float(delta[y]))
+        if margins_out is not None:
+            other = np.where(selected | np.isnan(cache if lazy else delta), -np.inf,
+                             cache if lazy else delta)
+            other[y] = -np.inf
+            margins_out.append(float(delta[y] - other.max()) if N > 1 else float("inf"))
         A.append(y)
         selected[y] = True
-        w = (cov[y] - W[:r].T @ W[:r, y]) / np.sqrt(diag[y] + jitter - W[:r, y] @ W[:r, y])
+        if log is not None:
+            log(r, y, float(delta[y]))
+        w = (sigma_row(y) - W[:r].T @ W[:r, y]) / np.sqrt(diag[y] + jitter - W[:r, y] @ W[:r, y])
         W[r] = w
         nom = nom - w * w
-        v = (Q[y] - V[:r].T @ V[:r, y]) / np.sqrt(prec[y])
+        v = (q_col(y) - V[:r].T @ V[:r, y]) / np.sqrt(prec[y])
         V[r] = v
         prec = prec - v * v
     return A

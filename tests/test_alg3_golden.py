@@ -39,6 +39,30 @@ def test_pinv_restatement_matches_reference_arithmetic(name):
     np.testing.assert_allclose(cache, z["cache"], rtol=1e-10, atol=1e-13)
 
 
+def test_pinv_restatement_at_c4_parameters_sampled():
+    """Config C4's own parameters (8^3, EQ, beta 4, cutoff 3) against the reference's arithmetic
+    directly, at a cost the CPU suite can carry: the pinv restatement's delta (tf_nominator /
+    tf_denominator, snippets_a2.py:138-213, threshold snippets_a2.py:480) for 24 sampled candidates
+    of round 0 (A = {}) and 24 of the first pick's window in round 1 (A = {a_0},
+    snippets_a3.py:196-308) equals the fixture's delta_cached_iters columns 0 and 1.  (The full
+    k = 24 run costs ~20 CPU-minutes; the precision form and the C oracle run it below.)"""
+    m, z = load("g888_eq_b4_c3")
+    cov, N = z["cov"], len(z["cov"])
+
+    def delta(y, A):
+        nom = op.tf_nominator(y, A, cov)
+        den = op.tf_denominator(y, [v for v in range(N) if v not in A], cov)
+        return 0.0 if (abs(den) < op.TF_SMALL or abs(nom) < op.TF_SMALL) else nom / den
+
+    rng = np.random.default_rng(0)
+    for y in rng.choice(N, 24, replace=False):
+        np.testing.assert_allclose(delta(int(y), []), z["dci"][y, 0], rtol=1e-10)
+    a0 = int(z["order"][0])
+    win = [y for y in op._window(a0, tuple(m["shape"]), m["cutoff"]) if y != a0]
+    for y in rng.choice(win, 24, replace=False):
+        np.testing.assert_allclose(delta(int(y), [a0]), z["dci"][y, 1], rtol=1e-10)
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_precision_form_matches_reference_arithmetic(name):
     m, z = load(name)

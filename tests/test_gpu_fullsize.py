@@ -9,7 +9,12 @@ there: its pinv greedy is O(N^4)).
   - the delta of each of the next picks equals nom / denom recomputed independently from Sigma
     and Q = Sigma^-1 columns: nom = sigma_yy - S_yA S_AA^-1 S_Ay and 1 / denom = Q_yy -
     Q_yA Q_AA^-1 Q_Ay (Schur complement of the precision over V \\ A);
-  - a second run is bit-identical.
+  - a second run is bit-identical;
+  - the whole 50-pick sequence EQUALS the CPU run of the same workload at N = 65,536
+    (tests/golden/bench65k_cpu_picks.json: LAPACK-blocked Cholesky + inverse on the host and the
+    oracle's incremental lazy greedy, tests/golden/make_golden_65k.py; smallest per-round margin
+    5.9e-7 relative), with every pick's delta within 1e-9 relative
+    (placement_algorithm2.py:151-219).
 * C3, N = 64^3, M = 512, minibatch 32,768: the analytic gradient of the negative ELBO agrees with a
   central difference of the GPU loss along a random direction of (amp, ls, noise, Z).
 """
@@ -94,6 +99,19 @@ def test_fullsize_delta_matches_schur_complements(split, r):
     Q = torch.stack([_q_col(L, S, j) for j in idx], 1)[idx].cpu().numpy()
     p_yy = Q[-1, -1] - Q[-1, :-1] @ np.linalg.solve(Q[:-1, :-1], Q[:-1, -1])
     np.testing.assert_allclose(split["dlt"][r], nom * p_yy, rtol=1e-7)
+
+
+def test_fullsize_picks_equal_cpu_fixture(split):
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                        "bench65k_cpu_picks.json")
+    with open(path) as f:
+        fx = json.load(f)
+    assert fx["N"] == split["N"] and fx["k"] == len(split["sel"])
+    assert split["sel"] == fx["picks"], next(
+        (r, a, b) for r, (a, b) in enumerate(zip(split["sel"], fx["picks"])) if a != b)
+    np.testing.assert_allclose(split["dlt"], fx["deltas"], rtol=1e-9)
 
 
 def test_fullsize_deterministic(split):

@@ -10,13 +10,17 @@
 //         -Wl,-rpath,$PWD/vgposp_amd -o tools/_build/step65k
 //   tools/_build/step65k tools/_build/x65k.bin [steps] [k]
 // Prints one JSON line: per-step time, the picks, and the library's own GEMM accounting
-// (launches, algorithmic flops, event time) of the last step.
+// (launches, algorithmic flops, event time) of the last step.  Progress goes to stderr through
+// unbuffered write(2) at every phase (library loaded, inputs uploaded, init enqueued, init
+// synchronised, every 10 rounds), so a profiled run that stalls shows where (verdict r5 item 5).
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "vgposp.h"
@@ -38,7 +42,21 @@
     }                                                                                  \
   } while (0)
 
+// One progress line on fd 2, unbuffered, with the seconds since start.
+static void progress(const char* what, int a = -1) {
+  static const auto t0 = std::chrono::steady_clock::now();
+  const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  char buf[160];
+  const int len = a >= 0 ? snprintf(buf, sizeof buf, "[step65k %8.3f s] %s %d\n", t, what, a)
+                         : snprintf(buf, sizeof buf, "[step65k %8.3f s] %s\n", t, what);
+  if (len > 0) {
+    const ssize_t w = write(2, buf, (size_t)len);
+    (void)w;
+  }
+}
+
 int main(int argc, char** argv) {
+  progress("start (library loaded by the dynamic linker)");
   if (argc < 2) {
     fprintf(stderr, "usage: step65k X.bin [steps] [k]\n");
     return 1;
@@ -74,26 +92,35 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dX, X.data(), X.size() * 8, hipMemcpyHostToDevice));
   const double par[3] = {amp, ls, noise};
   CK(hipMemcpy(dpar, par, 3 * 8, hipMemcpyHostToDevice));
+  progress("inputs uploaded, buffers allocated");
   hipStream_t s;
   CK(hipStreamCreate(&s));
-  auto step = [&]() {
+  auto step = [&](int it) {
     CV(vgposp_kernel_matrix(VGPOSP_KERNEL_EQ, dX, n, dX, n, (int)d, dpar, dpar + 1, dpar + 2, 1,
                             VGPOSP_FULL, dS, n, 0, s));
     CV(vgposp_greedy_init_ex(dS, n, n, k, 0.0, 1e-8, INFINITY, dinfo, ws, ws_bytes, s));
-    for (int r = 0; r < k; ++r)
+    progress("init enqueued, step", it);
+    CK(hipStreamSynchronize(s));
+    progress("init synchronised, step", it);
+    for (int r = 0; r < k; ++r) {
       CV(vgposp_greedy_step(dS, n, n, k, r, 1, dsel, dsel_delta, devals, ws, ws_bytes, s));
+      if (r % 10 == 9) {
+        CK(hipStreamSynchronize(s));
+        progress("rounds done:", r + 1);
+      }
+    }
   };
   double best = 1e30, total = 0.0;
   for (int it = 0; it < steps; ++it) {
     if (it + 1 == steps) vgposp_prof_enable(1);
     CK(hipStreamSynchronize(s));
     const auto t0 = std::chrono::steady_clock::now();
-    step();
+    step(it);
     CK(hipStreamSynchronize(s));
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     best = std::min(best, dt);
     total += dt;
-    fprintf(stderr, "step %d: %.3f s\n", it, dt);
+    fprintf(stderr, "step %d: %.3f s (with the progress synchronisations)\n", it, dt);
   }
   int info = 0;
   std::vector<int64_t> sel(k);

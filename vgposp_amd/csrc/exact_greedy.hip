@@ -55,7 +55,7 @@ constexpr int SEL_THREADS = 1024;
 // loads instead of picks -> X and slot_of_round -> boxlo chains.
 struct PickRec {
   int g[3];
-  int pad;
+  int pick;  // the pick's index: a record whose pick (or slot) differs from the round's is stale
   double x[3];
   long long lo[3];
   long long base;
@@ -1805,9 +1805,10 @@ __device__ void block_topb_entries(const double* cache, const unsigned char* sel
 #undef DBG_TB
 }
 
-__global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int nslots) {
+__global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int nslots, int kmax) {
   const int t = threadIdx.x;
   if (t < CTL_N) w.ctl[t] = t == CTL_STALL ? -1 : 0;
+  for (int r = t; r < kmax; r += blockDim.x) w.prec[r].pick = -1;  // no record of this run yet
   for (int i = t; i < nslots; i += blockDim.x) {
     w.rl_cand[i] = -1;
     w.rl_age[i] = 0;
@@ -1908,22 +1909,28 @@ struct StagedPicks {
 };
 
 // Picks 0 .. nA-1 (the whole workgroup calls it; the caller synchronises before use).  Picks
-// 0 .. nA-2 come from the workspace's pick records; pick nA-1 (this round's) is derived from
-// picks / X / slot_of_round / boxlo and, by workgroup 0, recorded for the rounds after.
+// 0 .. nA-2 come from the workspace's pick records when a record matches the round's pick and
+// slot; pick nA-1 (this round's), and any record that does not match (a round staged by no
+// earlier kernel of this run, e.g. through vgposp_exact_update), is derived from picks / X /
+// slot_of_round / boxlo.  Only workgroup 0, and only for pick nA-1, writes a record back: a
+// rebuilt older record stays private, so no workgroup can read one while it is written.
 __device__ __forceinline__ void stage_picks(const EArgs& a, const ExactWS& w,
                                             const long long* picks, int nA, StagedPicks& sp) {
   const long long bv = w.b0 * w.b1 * w.b2;
   for (int r = threadIdx.x; r < nA; r += blockDim.x) {
+    const long long i = picks[r];
+    const int slot = w.slot_of_round[r];
     PickRec pr;
+    bool ok = false;
     if (r + 1 < nA) {
       pr = w.prec[r];
-    } else {
-      const long long i = picks[r];
-      const int slot = w.slot_of_round[r];
+      ok = pr.pick == (int)i && pr.base == (long long)slot * bv;
+    }
+    if (!ok) {
       pr.g[0] = (int)(i / (a.I1 * a.I2));
       pr.g[1] = (int)((i / a.I2) % a.I1);
       pr.g[2] = (int)(i % a.I2);
-      pr.pad = 0;
+      pr.pick = (int)i;
       pr.x[0] = a.X[3 * i];
       pr.x[1] = a.X[3 * i + 1];
       pr.x[2] = a.X[3 * i + 2];
@@ -1931,7 +1938,7 @@ __device__ __forceinline__ void stage_picks(const EArgs& a, const ExactWS& w,
       pr.lo[1] = w.boxlo[3 * slot + 1];
       pr.lo[2] = w.boxlo[3 * slot + 2];
       pr.base = (long long)slot * bv;
-      if (blockIdx.x == 0) w.prec[r] = pr;
+      if (blockIdx.x == 0 && r + 1 == nA) w.prec[r] = pr;
     }
     for (int d = 0; d < 3; ++d) {
       sp.g[r][d] = pr.g[d];
@@ -3260,7 +3267,8 @@ extern "C" int vgposp_exact_bounds(VGPOSP_EXACT_PARAMS, const int* tab_off, cons
 extern "C" int vgposp_exact_steps_reset(VGPOSP_EXACT_PARAMS, void* stream) {
   VGPOSP_EXACT_PROLOGUE("vgposp_exact_steps_reset");
   (void)a;
-  hipLaunchKernelGGL(exact_steps_reset_kernel, dim3(1), dim3(256), 0, s, w, exact_slots(kmax));
+  hipLaunchKernelGGL(exact_steps_reset_kernel, dim3(1), dim3(256), 0, s, w, exact_slots(kmax),
+                     kmax);
   VG_LAUNCH_CHECK();
   return 0;
 }

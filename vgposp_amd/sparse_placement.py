@@ -623,17 +623,22 @@ class ExactWindowGreedy:
             call("vgposp_exact_pretighten", *args, *targs[:-1], int(self.pretighten), st)
         call("vgposp_exact_steps", *args, 0, 1, k, B, pk, pd, st)  # round 0 stalls: nothing refined
         issued, reads = 1, 0
-        # every host read either issues at least one new round or clears a stall by refining /
-        # tightening at least one candidate; each candidate is refined at most once per bound
-        # level, so a correct run needs far fewer reads than this cap
-        max_reads = k * (2 + REFINE_BATCH_MAX) + 16
+        # every host read must show progress since the previous one: the stall moved to another
+        # round, or candidates were refined (c[4]) or tightened (c[7]), or (no stall) more rounds
+        # were issued.  A read that shows none of these would repeat forever.  (Counting reads
+        # instead is wrong: recycled slots let a candidate be refined again, and stall events per
+        # round are not bounded by the batch size.)
+        prev = None
         while True:
             # stall round, CG batch, refined-unpicked, events, refined, age, tightening list, tightened
             c = ctl.cpu().tolist()
             reads += 1
-            if reads > max_reads:
-                raise RuntimeError(f"run_bounded: {reads} control-block reads for k = {k} "
-                                   f"(control block {c}): the device rounds are not progressing")
+            state = (c[0], c[4], c[7], issued)
+            if state == prev:
+                raise RuntimeError(f"run_bounded: control block {c} unchanged after the previous "
+                                   f"read ({reads} reads, k = {k}): the device rounds are not "
+                                   "progressing")
+            prev = state
             stall = c[0]
             if stall >= 0:
                 if c[1] == 0 and c[6] == 0:
