@@ -129,7 +129,11 @@ def cpu_baseline(args, N):
         naff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         naff = ncpu
-    for th in sorted({ncpu, naff}, reverse=True):
+    # numpy / scipy's OpenBLAS is built for at most 64 threads (MAX_THREADS=64): asking it for the
+    # box's 256 runs no faster and segfaulted inside OpenBLAS (round 6, the n = 4,096 sample), so
+    # the counts are capped there; 16 is one GPU's share of the box (its OMP_NUM_THREADS)
+    blas_max = 64
+    for th in sorted({min(ncpu, blas_max), min(naff, blas_max), min(16, ncpu)}, reverse=True):
         if threadpool_limits is not None:
             with threadpool_limits(limits=th, user_api="blas"):
                 t0 = time.perf_counter()
@@ -573,7 +577,8 @@ def c4_roofline(run, prof, ncand, pmc_path=None):
         per node (coefficient row, r / p / q / x reads and writes), every column counted for the
         iteration cap (columns that converge earlier exit early, so this over-counts).
     `traffic`: FETCH + WRITE bytes per run from a rocprofv3 PMC pass (profiles/pmc_c4_*.json) when
-    it was measured on this build's sources."""
+    it was measured on this build's sources.  The block returned leads with whichever of the two
+    took more time in the profiled run and nests the other ("cg" or "bounds")."""
     from vgposp_amd._lib import source_hash
     from vgposp_amd.sparse_placement import reach_table
     g = run.greedy
@@ -588,7 +593,7 @@ def c4_roofline(run, prof, ncand, pmc_path=None):
     out = {"kernel": "exact_bounds", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
            "achieved": uniq / (b_ms * 1e-3) / 1e9 if b_ms else None, "traffic": None,
            "algorithmic_bytes": uniq, "candidates": ncand, "K": K, "reach_nodes": T,
-           "l2_operand_bytes": oper,
+           "l2_operand_bytes": oper, "ms_per_run": b_ms,
            "l2_achieved": oper / (b_ms * 1e-3) / 1e9 if b_ms else None, "l2_peak": L2_PEAK_GBS}
     if out["achieved"]:
         out["frac"] = out["achieved"] / HBM_PEAK_GBS
@@ -604,6 +609,7 @@ def c4_roofline(run, prof, ncand, pmc_path=None):
     out["cg"] = {"kernel": "exact_cg_a/b", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                  "columns": g.refinements, "iterations": g.cg_iters, "batches": g.refine_batches,
                  "node_iterations_per_column": node_its, "algorithmic_bytes": cg_bytes,
+                 "ms_per_run": cg_ms, "traffic": None,
                  "achieved": cg_bytes / (cg_ms * 1e-3) / 1e9 if cg_ms else None,
                  "launch_bound_floor_ms": g.refine_batches * (2 * g.cg_iters + 2) * 6.5e-3}
     if out["cg"]["achieved"]:
@@ -623,6 +629,10 @@ def c4_roofline(run, prof, ncand, pmc_path=None):
             out["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         else:
             out["traffic_note"] = "null: the PMC file was measured on other kernel sources"
+    if cg_ms > b_ms:  # lead with the dominant phase
+        cg = out.pop("cg")
+        cg["bounds"] = out
+        return cg
     return out
 
 

@@ -1,6 +1,6 @@
 """Phase timing inside the C4 per-round kernels (A/B builds with -DVGPOSP_EXACT_DBG=1,
 tools/build_exact_variant.sh dbg -DVGPOSP_EXACT_DBG=1; run with
-VGPOSP_LIB=$PWD/tools/variants/lib_dbg.so python tools/exact_dbg.py [--one-level]).
+VGPOSP_LIB=$PWD/tools/variants/lib_dbg.so python tools/exact_dbg.py; the library from SRC=../../tools/variants/exact_greedy_dbg.hip tools/build_exact_variant.sh dbg -DVGPOSP_EXACT_DBG=1 [--one-level]).
 Prints the mean phase durations (us) of the stall kernel and the step kernel over one 128^3 run:
 stall: argmax | top-B | slot staging | slot ranking | batch write;
 step: window keys | argmax | slot lookup | pick + key refresh | factor rows;

@@ -1,5 +1,5 @@
 """Phase cycles of the 128-leaf Cholesky + inverse kernel (potrf_leaf_kernel) in a plain N = 8,192
-factorization, from a -DVGPOSP_STAMPS build (tools/build_potrf_variant.sh stamps -DVGPOSP_STAMPS;
+factorization, from a -DVGPOSP_STAMPS build (SRC=../../tools/variants/potrf_stamps.hip tools/build_potrf_variant.sh stamps -DVGPOSP_STAMPS;
 VGPOSP_LIB=$PWD/tools/variants/lib_stamps.so python tools/leaf_probe.py).  Thread 0 of every leaf
 workgroup accumulates s_memtime deltas: panel updates | panel factors | diagonal-block inverses |
 off-diagonal inverse chains | output; printed per leaf, in microseconds at the measured clock."""

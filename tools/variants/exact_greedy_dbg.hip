@@ -1,3 +1,8 @@
+// PHASE-STAMPED BUILD of vgposp_amd/csrc/exact_greedy.hip (not built into the library): the
+// product file as of round 5/6 with its -DVGPOSP_EXACT_DBG=1|2|3 instrumentation (thread 0 of the
+// per-round kernels stamps phases with s_memrealtime; vgposp_exact_dbg copies the last 64 records
+// out).  With VGPOSP_EXACT_DBG=0 it compiles to the same device code as the product file.
+// Build: SRC=../../tools/variants/exact_greedy_dbg.hip tools/build_exact_variant.sh dbg -DVGPOSP_EXACT_DBG=1
 // Exact algorithm 3 on the sparse tapered covariance (config C4): the rounds.
 //
 // snippets_a3.sparse_placement_algorithm_3 (snippets_a3.py:43-364) re-scores, after each pick y*,
@@ -1678,7 +1683,7 @@ __device__ __forceinline__ void topb_out(const long long* list, int B, long long
 
 template <int P, class KeyFn>
 __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long long* si,
-                               long long* out) {
+                               long long* out, unsigned long long* dt = nullptr) {
   const int t = threadIdx.x, wave = t >> 6;
   constexpr int NW = SEL_THREADS / 64;
   double v[P];
@@ -1704,6 +1709,7 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
   if (B > TOPW) {
     wave_topb<P>(v, id, TOPW, sv + wave * TOPW, si + wave * TOPW);
     __syncthreads();
+    if (dt != nullptr && t == 0) *dt = __builtin_amdgcn_s_memrealtime();  // (debug builds)
     if (wave == 0) {
       constexpr int Q1 = NW * TOPW / 64;  // items per lane; lanes 4s .. 4s + 3 hold wave s's
       static_assert(Q1 == 2 && TOPW == 8, "merge layout: two items per lane, four lanes per wave");
@@ -1762,7 +1768,10 @@ __device__ int block_topb_keys(int count, int B, KeyFn key, double* sv, long lon
 // candidates, best first (out[1] is the arg-max).  The whole workgroup calls it.
 __device__ void block_topb_entries(const double* cache, const unsigned char* sel, long long n,
                                    const ExactWS& w, long long nblk, long long nsb, int B,
-                                   long long* out) {
+                                   long long* out, unsigned long long* dt = nullptr) {
+  // (dt: debug builds with VGPOSP_EXACT_DBG=3 stamp the three levels, dt[1] .. dt[4])
+#define DBG_TB(k) \
+  if (dt != nullptr && threadIdx.x == 0) dt[k] = __builtin_amdgcn_s_memrealtime();
   constexpr int NW = SEL_THREADS / 64;
   __shared__ double sv[NW * CG_B + CG_B];
   __shared__ long long si[NW * CG_B + CG_B];
@@ -1780,12 +1789,14 @@ __device__ void block_topb_entries(const double* cache, const unsigned char* sel
     __syncthreads();
     return;
   }
+  DBG_TB(1)
   // blocks of those superblocks (their keys' candidates name them)
   const int nb = block_topb_keys<2>(ns * ESB, B, [&](int i, double& v, long long& k) {
     const long long b = (sbs[1 + i / ESB] / (EB * ESB)) * ESB + (i % ESB);
     v = b < nblk ? w.bval[b] : 0.0;
     k = b < nblk ? w.bidx[b] : -1;
   }, sv, si, blks);
+  DBG_TB(2)
   // entries of those blocks
   block_topb_keys<8>(nb * EB, B, [&](int i, double& v, long long& k) {
     const long long y = (blks[1 + i / EB] / EB) * EB + (i % EB);
@@ -1794,7 +1805,9 @@ __device__ void block_topb_entries(const double* cache, const unsigned char* sel
     const bool ok = y < n && !sel[yc];
     v = ok ? cv : 0.0;
     k = ok ? y : -1;
-  }, sv, si, out);
+  }, sv, si, out, dt != nullptr ? dt + 3 : nullptr);
+  DBG_TB(4)
+#undef DBG_TB
 }
 
 __global__ __launch_bounds__(256) void exact_steps_reset_kernel(ExactWS w, int nslots, int kmax) {
@@ -1817,8 +1830,33 @@ constexpr int EX_KMAX = 128;  // picks per run of the exact path (k = 50 in conf
 constexpr int EX_SLOTS_MAX = 2 * EX_KMAX;  // column slots (exact_slots(kmax) <= this)
 constexpr int ROWS_LDS = 8192;  // doubles: packed rows of both factors (each half) up to |A| = 90
 
-// (The phase-stamped build of this file, -DVGPOSP_EXACT_DBG=1/2/3 with vgposp_exact_dbg, is
-// tools/variants/exact_greedy_dbg.hip.)
+// (A/B builds only, -DVGPOSP_EXACT_DBG=1: thread 0 of the per-round kernels stamps its phases with
+// the 100 MHz real-time counter; vgposp_exact_dbg copies the last 64 records out.)
+#ifndef VGPOSP_EXACT_DBG
+#define VGPOSP_EXACT_DBG 0
+#endif
+#if VGPOSP_EXACT_DBG
+__device__ unsigned long long g_exact_dbg[64][8];
+__device__ unsigned int g_exact_dbg_n;
+#define DBG_DECL unsigned long long dbg_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define DBG_T(k) \
+  if (threadIdx.x == 0) dbg_t[k] = __builtin_amdgcn_s_memrealtime();
+#define DBG_END(kind)                                                         \
+  if (threadIdx.x == 0) {                                                     \
+    dbg_t[7] = (kind);                                                        \
+    const unsigned slot = atomicAdd(&g_exact_dbg_n, 1u) & 63u;                \
+    for (int q = 0; q < 8; ++q) g_exact_dbg[slot][q] = dbg_t[q];              \
+  }
+#else
+#define DBG_DECL
+#define DBG_T(k)
+#define DBG_END(kind)
+#endif
+#if VGPOSP_EXACT_DBG == 1
+#define DBG_END_STEP() DBG_END(2)
+#else
+#define DBG_END_STEP()
+#endif
 
 // Rows of chol(Q_AA) / chol(S_AA + eps I) as packed lower triangles (row r at r (r + 1) / 2), in
 // the workspace (P = const double*) or staged in LDS (P = an address-space-3 pointer, so the
@@ -2276,12 +2314,20 @@ __device__ __forceinline__ void window_tail(const EArgs& a, const double* __rest
                                             const ExactWS& w, int round, const long long* picks,
                                             const Window& v, const StagedPicks& sp, const R& L,
                                             RowsLds* lds) {
+  DBG_DECL
   const int nr = round + 1;
   const int wave = threadIdx.x >> 6;
+  DBG_T(0)
+  DBG_T(1)
   if (wave < 2) {
     wave_new_row<KIND>(a, w, round, L, sp, lds);
+    DBG_T(2)
+    DBG_T(3)
     __syncthreads();
+    DBG_T(4)
+    DBG_T(5)
     if (blockIdx.x == 0) {
+      DBG_END(3)
     }
     return;
   }
@@ -2465,7 +2511,11 @@ struct StepLds {
 
 __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
                                       const unsigned char* sel, const ExactWS& w, long long nblk,
-                                      long long nsb, long long at, StepLds& L) {
+                                      long long nsb, long long at, StepLds& L,
+                                      unsigned long long* dt = nullptr) {
+  // (dt: debug builds with VGPOSP_EXACT_DBG=2 stamp the phases here)
+#define DBG_PT(k) \
+  if (dt != nullptr && threadIdx.x == 0) dt[k] = __builtin_amdgcn_s_memrealtime();
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63, nwave = blockDim.x >> 6;
   if (nsb > SK_MAXNSB) return false;
   // level 1: the distinct blocks / superblocks of the window (wave 0, ALU and LDS only); the
@@ -2536,6 +2586,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     L.sidx[q] = w.sidx[q];
   }
   __syncthreads();
+  DBG_PT(1)
   if (!L.ok) return false;
   const int nb = L.nb, ns = L.ns;
   // level 2: the window blocks' entries (registers) — issued first, so that their round trip
@@ -2570,6 +2621,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     L.bidx[q][j] = b < nblk ? w.bidx[b] : -1;
   }
   __syncthreads();  // the LDS block keys are in place before the new ones overwrite them
+  DBG_PT(2)
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     if (q >= cnt) break;
@@ -2588,6 +2640,7 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     }
   }
   __syncthreads();
+  DBG_PT(3)
   for (int q = wave; q < ns; q += nwave) {
     double v = L.bval[q][lane];
     long long idx = L.bidx[q][lane];
@@ -2600,6 +2653,8 @@ __device__ bool block_window_keys_lds(const EArgs& a, const double* cache,
     }
   }
   __syncthreads();
+  DBG_PT(4)
+#undef DBG_PT
   return true;
 }
 
@@ -2660,26 +2715,44 @@ __device__ __forceinline__ void step_body(const EArgs& ea, double* cache, unsign
                                           const ExactWS& w, long long nblk, long long nsb,
                                           int nslots, int round, int rows, long long* picks,
                                           double* pick_delta, StepSm& sm, int& s_slot) {
+  DBG_DECL
+  DBG_T(0)
   if (w.ctl[CTL_STALL] >= 0) return;  // an earlier round is waiting for a refinement
   const long long n = ea.n;
   long long a;
   const long long prev = round > 0 ? picks[round - 1] : -1;
-  if (prev >= 0 && block_window_keys_lds(ea, cache, sel, w, nblk, nsb, prev, sm.k)) {
+#if VGPOSP_EXACT_DBG == 2
+  unsigned long long* dtp = dbg_t;
+#else
+  unsigned long long* dtp = nullptr;
+#endif
+  if (prev >= 0 && block_window_keys_lds(ea, cache, sel, w, nblk, nsb, prev, sm.k, dtp)) {
+#if VGPOSP_EXACT_DBG != 2
+    DBG_T(1)
+#endif
     a = block_argmax_lds(sm.k, nsb);
+#if VGPOSP_EXACT_DBG == 2
+    DBG_T(5)
+    DBG_END(2)
+    (void)0;
+#endif
   } else {
     if (prev >= 0) {  // (a window too large for the LDS lists; the pick's own block as well)
       block_window_keys(ea, cache, sel, w, nblk, prev);
       if (threadIdx.x < 64) wave_refresh_keys(cache, sel, w, n, nblk, prev);
       __syncthreads();
     }
+    DBG_T(1)
     a = block_argmax(w, nsb);
   }
+  DBG_T(2)
   if (threadIdx.x == 0) s_slot = -1;
   __syncthreads();
   if (a >= 0)
     for (int i = threadIdx.x; i < nslots; i += SEL_THREADS)
       if (w.rl_cand[i] == a) s_slot = i;
   __syncthreads();
+  DBG_T(3)
   const int slot = s_slot;
   if (a < 0 || slot >= 0) {  // pick (no candidate left: picks[round] = -1, nothing changes)
     if (threadIdx.x == 0) {
@@ -2694,7 +2767,10 @@ __device__ __forceinline__ void step_body(const EArgs& ea, double* cache, unsign
       }
     }
     __syncthreads();
+    DBG_T(4)
     if (a >= 0 && rows) block_factor_rows<KIND>(ea, w, round, picks, sm.r);
+    DBG_T(5)
+    DBG_END_STEP()
     return;
   }
   // stall: the batch is chosen by exact_stall_kernel, which the host launches first thing in
@@ -2746,14 +2822,27 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
                                                                   int nslots, int B) {
   __shared__ long long top[CG_B + 1];
   __shared__ long long s_todo[CG_B];
+  DBG_DECL
+  DBG_T(0)
   if (w.ctl[CTL_STALL] < 0) return;
   const long long a = block_argmax(w, nsb);
+#if VGPOSP_EXACT_DBG != 3
+  DBG_T(1)
+#endif
   // stall: the B best entries without a column become the refinement batch.  The slot table is
   // staged in LDS and ranked in parallel (a first version walked it with thread 0's dependent
   // global loads: 750 us per stall at B = 32): free slots are taken first, lowest index first,
   // then the unpinned ones, oldest refinement first — the candidates in the batch have no column,
   // so no slot of theirs can be recycled.
+#if VGPOSP_EXACT_DBG == 3
+  DBG_T(0)
+  block_topb_entries(cache, sel, n, w, nblk, nsb, B, top, dbg_t);
+  DBG_T(5)
+  DBG_END(1)
+#else
   block_topb_entries(cache, sel, n, w, nblk, nsb, B, top);
+#endif
+  DBG_T(2)
   __shared__ long long s_cand[EX_SLOTS_MAX];
   __shared__ int s_age[EX_SLOTS_MAX], s_inv_free[EX_SLOTS_MAX], s_inv_old[EX_SLOTS_MAX];
   __shared__ unsigned char s_pin[EX_SLOTS_MAX];
@@ -2773,6 +2862,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
   if (t == CG_B && a >= 0) s_qx[CG_B] = w.qexact[a];
   if (t == 0) s_nfree = s_nold = 0;
   __syncthreads();
+  DBG_T(3)
   for (int e = t; e < nslots * ntop; e += SEL_THREADS) {
     const int i = e / ntop, b = e % ntop;
     if (s_cand[i] >= 0 && s_cand[i] == top[1 + b]) s_has[b] = 1;
@@ -2794,6 +2884,7 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
     }
   }
   __syncthreads();
+  DBG_T(4)
   if (t < 64) {
     // without a column: a candidate still on its K_lo bound is tightened (K_hi bound, cheap); one
     // already tightened (or exact but recycled), and the arg-max itself, gets its CG column (the
@@ -2843,6 +2934,10 @@ __global__ __launch_bounds__(SEL_THREADS) void exact_stall_kernel(double* cache,
       w.ctl[CTL_NB] = nb;
     }
   }
+  DBG_T(5)
+#if VGPOSP_EXACT_DBG != 3
+  DBG_END(1)
+#endif
 }
 
 }  // namespace vgposp
@@ -3057,6 +3152,14 @@ int exact_refine_t(const EArgs& a, double* qdiag, double* cache, unsigned char* 
                              tau, ntau, kmax, cutoff);                                           \
   hipStream_t s = as_stream(stream)
 
+#if VGPOSP_EXACT_DBG
+extern "C" int vgposp_exact_dbg(unsigned long long* out) {  // 64 x 8 records, then reset
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(vgposp::g_exact_dbg), sizeof(vgposp::g_exact_dbg));
+  const unsigned z = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(vgposp::g_exact_dbg_n), &z, sizeof(z));
+  return 0;
+}
+#endif
 
 extern "C" size_t vgposp_exact_workspace_bytes(int64_t I0, int64_t I1, int64_t I2, int m, int kmax,
                                                int radius, int cg_iters) {

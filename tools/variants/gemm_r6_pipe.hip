@@ -371,6 +371,28 @@ __device__ __forceinline__ void gemm_pipe_loop(const GemmParams& p, const double
   // SPLIT: eight single ds_read_b64 (a read that crosses the loop's back edge: paired reads land
   // in register tuples the loop header does not use, and the copies into its registers wait for
   // the reads, exposing their latency)
+#ifdef VGPOSP_GEMM_VSTAGE
+  // register staging of the steady-state pieces: global_load_dwordx4 into R at the tile's barrier,
+  // ds_write_b128 into the free stage one tile later (slice 2), instead of LDS-DMA
+  double2 R[2 * PO];
+  auto vsrc = [&](int tt, int q) -> const double2* {
+    const int i = wave * PO + q % PO;
+    const int64_t k0 = kbeg + (int64_t)tt * GBK;
+    const bool kc = q < PO ? A_KC : B_KC;
+    const double* base = q < PO ? gA : gB;
+    const int64_t ld = q < PO ? p.lda : p.ldb, r0 = q < PO ? m0 : n0, Rr = q < PO ? p.m : p.n;
+    const double* src;
+    if (kc) {
+      const int row = 8 * i + (lane >> 3);
+      const int kp = (lane & 7) ^ ((row & 15) >> 1);
+      src = base + min(r0 + row, Rr - 1) * ld + min(k0 + 2 * kp, p.k - 2);
+    } else {
+      const int pp = lane ^ ((i & 1) << 3);
+      src = base + min(k0 + i, p.k - 1) * ld + min(r0 + 2 * pp, Rr - 2);
+    }
+    return reinterpret_cast<const double2*>(src);
+  };
+#endif
   auto read = [&](int st, int ks, double (&a)[4], double (&b)[FJ], auto SPLITc) {
     const double* As = smem + st * SE;
     const double* Bs = As + OPND_ELEMS;
@@ -430,9 +452,29 @@ __device__ __forceinline__ void gemm_pipe_loop(const GemmParams& p, const double
       }
       if (ks < 3) {
         read(t & 1, ks + 1, fa[c ^ 1], fb[c ^ 1], PAIRED{});
+#ifdef VGPOSP_GEMM_VSTAGE
+        if (ks == 2 && t >= 1 && more) {  // tile t + 1's pieces (loaded at tile t - 1's barrier)
+#pragma unroll
+          for (int q = 0; q < 2 * PO; ++q) {
+            const int i = wave * PO + q % PO;
+            double* dst = smem + ((t + 1) & 1) * SE + (q < PO ? 0 : OPND_ELEMS) + i * 128 + 2 * lane;
+            *reinterpret_cast<double2*>(dst) = R[q];
+          }
+        }
+#endif
       } else if (more) {
         // every wave's reads of this stage are done (the wait above) and its pieces of tile t + 1
         // have landed
+#ifdef VGPOSP_GEMM_VSTAGE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // this wave's writes landed
+        __builtin_amdgcn_s_barrier();
+        read((t + 1) & 1, 0, fa[c ^ 1], fb[c ^ 1], SPLIT{});
+        if (more2) {
+#pragma unroll
+          for (int q = 0; q < 2 * PO; ++q) R[q] = *vsrc(t + 2, q);
+        }
+        if (false) {
+#else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifndef VGPOSP_GEMM_EXP_NOBAR
         __builtin_amdgcn_s_barrier();
@@ -444,10 +486,13 @@ __device__ __forceinline__ void gemm_pipe_loop(const GemmParams& p, const double
 #else
         if (false) {
 #endif
+#endif
 #pragma unroll
           for (int q = 0; q < 2 * PO; ++q) issue_piece(t + 2, q);
         }
+#ifndef VGPOSP_GEMM_VSTAGE
         read((t + 1) & 1, 0, fa[c ^ 1], fb[c ^ 1], SPLIT{});
+#endif
       }
       __builtin_amdgcn_sched_barrier(0);
       // GEMM_SPREAD 1: tile t + 2's 8 pieces one per 2 MFMAs of slice 3; 2: pieces 0-3 one per 4

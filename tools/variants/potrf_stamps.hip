@@ -1,3 +1,7 @@
+// PHASE-STAMPED BUILD of vgposp_amd/csrc/potrf.hip (not built into the library): the product file
+// with its -DVGPOSP_STAMPS instrumentation (vgposp_potrf_stamps; tools/leaf_probe.py).  Without the
+// switch it compiles to the same device code as the product file.
+// Build: SRC=../../tools/variants/potrf_stamps.hip tools/build_potrf_variant.sh stamps -DVGPOSP_STAMPS
 // Recursive Cholesky (lower, in place) and recursive triangular inverse, built so that nearly all
 // flops land in large-K fp64 MFMA GEMMs (gemm.hip):
 //
@@ -49,8 +53,25 @@ constexpr int NB = 128;        // leaf size (== GEMM tile, so trsm leaves are in
 // ---------------------------------------------------------------------------------------------
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
-// (The phase-stamped build of this file, -DVGPOSP_STAMPS with vgposp_potrf_stamps, is
-// tools/variants/potrf_stamps.hip; tools/leaf_probe.py reads it.)
+// Phase stamps for tools/diag_probe.hip (debug builds only; compiled out otherwise).
+#ifdef VGPOSP_STAMPS
+__device__ long long g_stamps[16];
+}  // namespace vgposp
+// (debug builds: the accumulated phase cycles, then cleared; tools/leaf_probe.py)
+extern "C" int vgposp_potrf_stamps(long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgposp::g_stamps), sizeof(long long) * 16) != hipSuccess)
+    return 1;
+  long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(vgposp::g_stamps), z, sizeof(z)) == hipSuccess ? 0 : 1;
+}
+namespace vgposp {
+#define STAMP_NOW() ((long long)__builtin_amdgcn_s_memtime())
+#define STAMP_ADD(i, t0) \
+  if (threadIdx.x == 0) g_stamps[i] += STAMP_NOW() - (t0)
+#else
+#define STAMP_NOW() 0LL
+#define STAMP_ADD(i, t0)
+#endif
 
 constexpr int LW = 16;                 // panel width
 constexpr int LP2 = NB + 4;            // LDS pitch (doubles)
@@ -172,6 +193,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
     for (int c = t; c < JP; c += LEAF_THREADS) rdiag[c] = c < jb ? 1.0 / A[(int64_t)c * lda + c] : 1.0;
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
+  long long ts = STAMP_NOW();
 
   // Left-looking over 16-column panels:
   //   A[c0:, c0:c0+16] -= L[c0:, :c0] L[c0:c0+16, :c0]^T   (MFMA, 16-row tiles over the 4 waves)
@@ -199,6 +221,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
       }
       __syncthreads();
     }
+    STAMP_ADD(3, ts);
+    ts = STAMP_NOW();
     if (wave == 0) {
       const int r0 = c0 + lane, r1 = c0 + 64 + lane;
       const bool tall = JP - c0 > 64;
@@ -217,6 +241,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
       }
     }
     __syncthreads();
+    STAMP_ADD(1, ts);
+    ts = STAMP_NOW();
   }
 
   if (invert || linv) {
@@ -242,6 +268,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
       }
     }
     __syncthreads();
+    STAMP_ADD(2, ts);
+    ts = STAMP_NOW();
     // Off-diagonal blocks, one block column per chain: X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj for
     // i = j+1 .. NP-1 depends only on block column j, so a wave owns whole columns (j and
     // NP-1-j: balanced work for NP <= 8) and needs wave-level ordering only.
@@ -289,6 +317,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
     }
     __syncthreads();
   }
+  STAMP_ADD(4, ts);
+  ts = STAMP_NOW();
 
   for (int e = t; e < NB * NB; e += LEAF_THREADS) {
     const int r = e / NB, c = e % NB;
@@ -300,6 +330,8 @@ __global__ __launch_bounds__(LEAF_THREADS) void potrf_leaf_kernel(double* A, int
   if (diag_out != nullptr) {
     for (int c = t; c < jb; c += LEAF_THREADS) diag_out[c] = L[c * LP2 + c];
   }
+  STAMP_ADD(5, ts);
+  (void)ts;
 }
 
 static size_t leaf_shmem() { return (size_t)NB * LP2 * sizeof(double); }
