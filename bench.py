@@ -67,11 +67,11 @@ def parse():
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only to rehearse "
                         "the multi-rank path on one GPU with VGPOSP_BENCH_DEVICE=0)")
-    p.add_argument("--c4-pmc", default=os.path.join(ROOT, "profiles", "pmc_c4_r5.json"),
+    p.add_argument("--c4-pmc", default=os.path.join(ROOT, "profiles", "pmc_c4_r6.json"),
                    help="per-run C4 kernel bytes from rocprofv3 PMC passes (tools/pmc_c4.py)")
     p.add_argument("--rank-check", action="store_true",
                    help="(tests) every rank prints its rank / world size and exits before any GPU call")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r5.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r6.json"),
                    help="per-launch HBM bytes from a rocprofv3 PMC pass of this command")
     return p.parse_args()
 

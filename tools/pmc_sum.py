@@ -4,7 +4,8 @@
 Per family: dispatches, the counters summed over its dispatches, and derived fractions where the
 counters are present — SQ_* wave-cycle shares (WAIT_ANY / WAIT_INST_ANY / ACTIVE_INST_ANY of
 WAVE_CYCLES), instructions per wave-cycle, and SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x 4
-SIMDs x CUs) (the MFMA-busy fraction of the dispatches' GPU-active cycles)."""
+SIMDs x CUs / 8) (GRBM_GUI_ACTIVE is summed over the 8 XCDs; the MFMA-busy fraction of the
+dispatches' GPU-active cycles, as tools/pmc_gemm_step.py)."""
 import argparse
 import csv
 import json
@@ -46,7 +47,7 @@ def main():
                 if k in c:
                     r[k.lower() + "_per_wave_cycle"] = c[k] / wc
         if "SQ_VALU_MFMA_BUSY_CYCLES" in c and c.get("GRBM_GUI_ACTIVE"):
-            r["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] * 4 * a.cus)
+            r["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 4 * a.cus)
         res[fam] = r
     with open(a.out, "w") as f:
         json.dump({"command": a.command, "note": a.note, "kernels": res}, f, indent=1)
