@@ -117,9 +117,10 @@ def cpu_baseline(args, N):
 
     shape = (16, 16, 32)
     S = sigma(shape)
-    # all the host's logical CPUs (OPENBLAS_NUM_THREADS = os.cpu_count()), and the
-    # CPUs this process may run on (the GPU box gives each GPU a share of the machine)
-    runs = {}
+    # the host's CPUs, capped at 64: numpy / scipy's OpenBLAS is built for at most 64 threads
+    # (MAX_THREADS=64), so asking it for the box's 256 runs no faster.  ONE thread count for the
+    # whole leg: changing OpenBLAS's count back up inside the process (64 -> 16 -> 64) segfaulted
+    # it in round 6 (tools/cpu_blas_probe.py runs each count in its own process without a fault)
     try:
         from threadpoolctl import threadpool_limits
     except ImportError:  # pragma: no cover
@@ -129,37 +130,19 @@ def cpu_baseline(args, N):
         naff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         naff = ncpu
-    # numpy / scipy's OpenBLAS is built for at most 64 threads (MAX_THREADS=64): asking it for the
-    # box's 256 runs no faster and segfaulted inside OpenBLAS (round 6, the n = 4,096 sample), so
-    # the counts are capped there; 16 is one GPU's share of the box (its OMP_NUM_THREADS)
-    blas_max = 64
-    for th in sorted({min(ncpu, blas_max), min(naff, blas_max), min(16, ncpu)}, reverse=True):
-        if threadpool_limits is not None:
-            with threadpool_limits(limits=th, user_api="blas"):
-                t0 = time.perf_counter()
-                op.placement_lazy_incremental(S, args.k)
-                runs[th] = time.perf_counter() - t0
-        else:
-            t0 = time.perf_counter()
-            op.placement_lazy_incremental(S, args.k)
-            runs[cpu_threads()] = time.perf_counter() - t0
-    del S
-    th_main = max(runs)
-    t_inc = runs[th_main]
-    # a second, smaller sample at the same thread count, for a two-point a n^3 + b n^2 model of
-    # the time (the O(n^3) init and the O(n^2) rounds) extrapolated to the headline's N
-    shape_s = (16, 16, 16)
-    S = sigma(shape_s)
+    th_main = min(naff, 64)
+    # (set once here and never restored inside the leg: the pinv sample and the Cholesky below
+    # run at the same count)
     if threadpool_limits is not None:
-        with threadpool_limits(limits=th_main, user_api="blas"):
-            t0 = time.perf_counter()
-            op.placement_lazy_incremental(S, args.k)
-            t_small = time.perf_counter() - t0
-    else:
-        t0 = time.perf_counter()
-        op.placement_lazy_incremental(S, args.k)
-        t_small = time.perf_counter() - t0
+        threadpool_limits(limits=th_main, user_api="blas")
+    parts = {}
+    t0 = time.perf_counter()
+    op.placement_lazy_incremental(S, args.k, timings=parts)
+    t_inc = time.perf_counter() - t0
     del S
+    if threadpool_limits is None:  # pragma: no cover
+        th_main = cpu_threads()
+    runs = {th_main: t_inc}
     ps = tuple(args.cpu_shape)
     Sp = sigma(ps)
     trace = []
@@ -177,12 +160,10 @@ def cpu_baseline(args, N):
     np.linalg.cholesky(Sc)
     tc = time.perf_counter() - t0
     n_inc = int(np.prod(shape))
-    n_s = int(np.prod(shape_s))
-    # t(n) = a n^3 + b n^2 through (n_s, t_small) and (n_inc, t_inc)
-    den = n_inc ** 3 * n_s ** 2 - n_s ** 3 * n_inc ** 2
-    a3 = (t_inc * n_s ** 2 - t_small * n_inc ** 2) / den
-    b2 = (t_small * n_inc ** 3 - t_inc * n_s ** 3) / den
-    t_fit = a3 * N ** 3 + b2 * N ** 2
+    # the sample's two parts scaled by their own orders: the O(n^3) factor + inverse by (N / n)^3,
+    # the O(k n^2) rounds (and the sample's fixed costs) by (N / n)^2
+    f3, f2 = (N / n_inc) ** 3, (N / n_inc) ** 2
+    t_fit = parts["factor_inverse"] * f3 + (t_inc - parts["factor_inverse"]) * f2
     return {
         "value": args.k / t_inc,
         "unit": "placements/s",
@@ -197,17 +178,20 @@ def cpu_baseline(args, N):
                    f"{(N / n_inc) ** 3:.0f}x this sample's"),
         "gpu_same_sample": gpu_same,
         # the headline's own config is N = 65,536 (timing it there takes most of an hour of host
-        # time: tests/golden/make_golden_65k.py).  Scaling the WHOLE sample time by (N / n)^3
-        # over-scales its O(n^2) rounds and fixed costs, and BLAS runs faster at large n, so that
-        # time is too long and its rate a LOWER bound of the CPU's rate at the config; the
-        # two-point fit a n^3 + b n^2 (samples n = 4,096 and 8,192) is the estimate
+        # time).  Scaling the WHOLE sample time by (N / n)^3 over-scales its O(n^2) rounds and
+        # fixed costs, and BLAS runs faster at large n, so that time is too long and its rate a
+        # LOWER bound of the CPU's rate at the config; the estimate scales each part by its order
         "at_config_lower_bound": {
             "value": args.k / (t_inc * (N / n_inc) ** 3), "unit": "placements/s", "N": N,
             "model": f"whole sample time x (N / {n_inc})^3 (a lower bound of the rate)"},
         "at_config_estimate": {
-            "value": args.k / t_fit if t_fit > 0 else None, "unit": "placements/s", "N": N,
-            "model": (f"t(n) = a n^3 + b n^2 through n = {n_s} ({t_small:.2f} s) and n = {n_inc} "
-                      f"({t_inc:.2f} s): a = {a3:.3e}, b = {b2:.3e}, t({N}) = {t_fit:.0f} s")},
+            "value": args.k / t_fit, "unit": "placements/s", "N": N,
+            "model": (f"factor + inverse {parts['factor_inverse']:.2f} s x (N / {n_inc})^3 + rounds "
+                      f"and the rest {t_inc - parts['factor_inverse']:.2f} s x (N / {n_inc})^2 = "
+                      f"{t_fit:.0f} s")},
+        # measured at the config itself, on another host: the oracle's algorithm on the bench's
+        # exact workload, in the build container (tests/golden/bench65k_cpu_picks.json)
+        "at_config_measured": _cpu_fixture_rate(),
         "reference_algorithm": {
             "value": args.cpu_k / t_pinv, "unit": "placements/s",
             "sample": (f"pinv restatement of placement_algorithm2.placement_algorithm_2 on a "
@@ -218,6 +202,23 @@ def cpu_baseline(args, N):
         "cholesky_sample": f"numpy.linalg.cholesky at N={nc}",
         "cpu_model": cpu_model(),
     }
+
+
+def _cpu_fixture_rate():
+    """placements/s of the host run that made tests/golden/bench65k_cpu_picks.json (the bench's
+    own N = 65,536 workload, the oracle's algorithm; the build container, not the GPU box)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "bench65k_cpu_picks.json")) as f:
+            fx = json.load(f)
+    except (OSError, ValueError):
+        return None
+    t = fx["times"]
+    secs = t["cholesky_inverse_s"] + t["diag_q_s"] + t["rounds_s"]
+    return {"value": fx["k"] / secs, "unit": "placements/s", "N": fx["N"], "seconds": secs,
+            "host": f"the build container, {fx.get('blas_threads')} OpenBLAS threads (blocked "
+                    "Cholesky + inverse, then the incremental lazy rounds; Sigma's assembly "
+                    f"({t['assemble_s']} s) excluded); its picks are the ones the main line's "
+                    "matches_committed_picks compares with"}
 
 
 def gpu_on_sample(S, k, reps=5):

@@ -236,7 +236,7 @@ def _lazy_select_np(cache, fresh_delta, selected):
 
 
 def placement_lazy_incremental(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, cache_init=np.inf,
-                               deltas_out=None):
+                               deltas_out=None, timings=None):
     """placement_lazy_precision with O(N^3) once + O(N^2) per round, for N ~ 16k (the GPU test of a
     full k = 50 sequence).  Same deltas, rank-1 updated instead of re-factored:
       nom_y  = sigma_yy - |W[:, y]|^2,  W[t] = (Sigma_{a_t,:} - W^T W[:, a_t]) / sqrt(pivot_t)
@@ -245,7 +245,10 @@ def placement_lazy_incremental(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, 
                sqrt(P_{a_t a_t}): removing a_t from S = V \\ A downdates (Sigma_SS + eps I)^-1;
       denom_y = 1 / P_yy - eps.
     Pinned against placement_lazy_precision and the reference goldens in tests/test_oracle.py."""
+    import time
+
     from scipy.linalg import lapack
+    t0 = time.perf_counter()
     cov = np.asarray(cov_vv, dtype=np.float64)
     N = cov.shape[0]
     Mj = cov.copy()
@@ -258,9 +261,13 @@ def placement_lazy_incremental(cov_vv, k, lazy=True, jitter=0.0, thr=DELTA_EPS, 
         raise np.linalg.LinAlgError(f"dpotri info {info}")
     del c, Mj
     Q = np.tril(Q) + np.tril(Q, -1).T
-    return placement_lazy_columns(np.diag(cov).copy(), lambda y: cov[y], np.diag(Q).copy(),
-                                  lambda y: Q[y], k, lazy=lazy, jitter=jitter, thr=thr,
-                                  cache_init=cache_init, deltas_out=deltas_out)
+    t1 = time.perf_counter()
+    A = placement_lazy_columns(np.diag(cov).copy(), lambda y: cov[y], np.diag(Q).copy(),
+                               lambda y: Q[y], k, lazy=lazy, jitter=jitter, thr=thr,
+                               cache_init=cache_init, deltas_out=deltas_out)
+    if timings is not None:  # the O(N^3) factor + inverse and the O(k N^2) rounds, in seconds
+        timings.update(factor_inverse=t1 - t0, rounds=time.perf_counter() - t1)
+    return A
 
 
 def placement_lazy_columns(sigma_diag, sigma_row, q_diag, q_col, k, lazy=True, jitter=0.0,
