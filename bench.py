@@ -475,7 +475,8 @@ def c4_line(args, world, rank, barrier, maxtime):
                                   "exact algorithm 3 (dense-equivalent deltas, TF constants)",
                       "N": int(np.prod(shape)), "k": k,
                       "parallelism": "single" if world == 1 else
-                      f"bounds sharded over {world} ranks (one all-gather), rounds replicated"},
+                      f"bounds sharded over {world} ranks (one all-gather), rounds replicated "
+                      "(profiles/r6_c4_shard_model.json)"},
            "method": "bounded-lazy (K-step CG brackets of Q_yy, refinement by CG columns)",
            "picks_head": picks[:6],
            "deterministic_selection": same,
