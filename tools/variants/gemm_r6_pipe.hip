@@ -303,14 +303,15 @@ __device__ __forceinline__ int tri_root(int64_t id) {
 // workgroups per CU.  (The 256x128 configurations measured against it live in
 // tools/variants/gemm_experiments.hip.)
 template <int CFG> struct GemmCfg {
-  static_assert(CFG == 1 || CFG == 4, "the 128x128 configurations built into the library");
+  static_assert(CFG == 1 || CFG == 4 || CFG == 5, "the 128x128 configurations");
   static constexpr int NSUB = 1;              // 128-row A sub-tiles
-  static constexpr int NW = CFG == 4 ? 8 : 4; // waves (CFG 4: 2 x 4 waves of 64 x 32)
+  // waves (CFG 4: 2 x 4 waves of 64 x 32; CFG 5: 2 x 2 computing waves of 64 x 64 + a loader)
+  static constexpr int NW = CFG == 4 ? 8 : CFG == 5 ? 5 : 4;
   static constexpr int FI = 4;                // 16-row fragments per wave
   static constexpr int FJ = CFG == 4 ? 2 : 4; // 16-column fragments per wave
   static constexpr int NST = STAGES;          // ring depth
   // the launch bound: minimum waves per SIMD (two workgroups per CU either way)
-  static constexpr int OCC = CFG == 4 ? 4 : GEMM_OCC;
+  static constexpr int OCC = CFG == 4 ? 4 : CFG == 5 ? 3 : GEMM_OCC;
 };
 
 // LDS of one workgroup of the fast kernel (doubles): the STAGES-deep ring of A sub-tiles | B.
@@ -519,6 +520,79 @@ __device__ __forceinline__ void gemm_pipe_loop(const GemmParams& p, const double
   }
 }
 
+// CFG 5: a LOADER wave (wave 4) issues all 32 LDS-DMA pieces of every K-tile, so the four
+// computing waves issue only fragment reads, MFMAs and one barrier per K-tile (an LDS-DMA
+// instruction blocks its wave's next MFMA issue: §4 "Round 6").  Barrier B_t: tile t is in stage
+// t % 2 and every computing wave has finished tile t - 1, so the loader then fills stage
+// (t + 1) % 2 with tile t + 1 and waits for it before B_{t+1}.  T barriers on both sides; the
+// loader exits after its last (an ended wave leaves the workgroup barrier).
+template <bool A_KC, bool B_KC, bool TA, bool TB, bool TRIA, bool TRIB>
+__device__ __forceinline__ void gemm_loader_loop(const GemmParams& p, const double* gA,
+                                                 const double* gB, int64_t m0, int64_t n0,
+                                                 int64_t kbeg, int64_t kend, int T,
+                                                 bool partial_last, double* smem,
+                                                 dbl4 (&acc)[4][4]) {
+  constexpr int SE = 2 * OPND_ELEMS;
+  if (T == 0) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave == 4) {
+    auto fill = [&](int tt) {
+      double* st = smem + (tt & 1) * SE;
+      const int64_t k0 = kbeg + (int64_t)tt * GBK;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) glds_piece<A_KC>(gA, p.lda, m0, k0, p.m, p.k, st, i, lane);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        glds_piece<B_KC>(gB, p.ldb, n0, k0, p.n, p.k, st + OPND_ELEMS, i, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    fill(0);
+    __builtin_amdgcn_s_barrier();  // B_0
+    for (int t = 0; t + 1 < T; ++t) {
+      fill(t + 1);
+      __builtin_amdgcn_s_barrier();  // B_{t+1}
+    }
+    return;
+  }
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int t = 0; t < T; ++t) {
+    __builtin_amdgcn_s_barrier();  // B_t
+    const double* As = smem + (t & 1) * SE;
+    const double* Bs = As + OPND_ELEMS;
+    const int64_t k0 = kbeg + (int64_t)t * GBK;
+    const bool mask = (partial_last && t == T - 1) || (TRIA && k0 < m0 + GBM && k0 + GBK > m0) ||
+                      (TRIB && k0 < n0 + GBN && k0 + GBK > n0);
+#pragma unroll
+    for (int ks = 0; ks < GBK / 4; ++ks) {
+      const int k = ks * 4 + fk;
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[frag_off<A_KC>(wm * 64 + i * 16 + fr, k)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[frag_off<B_KC>(wn * 64 + j * 16 + fr, k)];
+      if (mask) {
+        const int64_t gk = k0 + k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t gm = m0 + wm * 64 + i * 16 + fr;
+          if (gk >= kend || (TRIA && (TA ? gm > gk : gk > gm))) a[i] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t gn = n0 + wn * 64 + j * 16 + fr;
+          if (gk >= kend || (TRIB && (TB ? gk > gn : gn > gk))) b[j] = 0.0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
 // One workgroup of the fast kernel: workgroup `bid` of the launch's `nwg` for this problem, batch
 // element bz, LDS ring at smem (the kernel's own __shared__ array).
 template <bool TA, bool TB, bool TRIA, bool TRIB, int CFG>
@@ -574,7 +648,8 @@ __device__ __forceinline__ void gemm_glds_body(const GemmParams& p, int tiles_m,
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int wm = wave / (NW / 2), wn = wave % (NW / 2);
+  constexpr int NWC = CFG == 5 ? 4 : NW;  // computing waves
+  const int wm = wave / (NWC / 2), wn = wave % (NWC / 2);
   const int fr = lane & 15, fk = lane >> 4;
 
   // K range that can contribute when an operand is stored lower triangular.
@@ -602,7 +677,11 @@ __device__ __forceinline__ void gemm_glds_body(const GemmParams& p, int tiles_m,
 #pragma unroll
     for (int j = 0; j < FJ; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
 
-  if constexpr (GEMM_PIPE || CFG == 4) {
+  if constexpr (CFG == 5) {
+    gemm_loader_loop<A_KC, B_KC, TA, TB, TRIA, TRIB>(p, gA, gB, m0, n0, kbeg, kend, T,
+                                                      partial_last, smem, acc);
+    if (wave == 4) return;  // the loader stores nothing
+  } else if constexpr (GEMM_PIPE || CFG == 4) {
     gemm_pipe_loop<A_KC, B_KC, TA, TB, TRIA, TRIB, NW, FJ>(p, gA, gB, m0, n0, kbeg, kend, T,
                                                             partial_last, smem, acc);
   } else {
