@@ -3,7 +3,7 @@
 # (Profiles: tools/profile_r2.sh, tools/pmc_gemm_step.sh, tools/gpu_vgp_timeline.sh.)
 set -e
 R=${GRAFT_REPO_ROOT:-$PWD}
-O=$R/gpurun_out/r5end
+O=$R/gpurun_out/${ROUND_END_TAG:-r6end}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
