@@ -24,18 +24,26 @@ class LocalDist(DistCholesky):
         super().__init__(ops, dist_min=dist_min)
         self.rank, self.world = rank, world
 
-    def _exchange(self, pieces):
+    def _exchange(self, pieces, defer=None, depth=0):
+        """DistCholesky._exchange without the collective: rank r's pack, the same buffers, and the
+        unpack of the (unfilled) receive buffer at the same point — right away, or, for a
+        deferred exchange, at the _flush that the real code waits in."""
         ops = self.ops
         sizes = [ops.pack_elems(*p) for p in pieces]
         S = max(sizes)
-        send = self._buf("send", S, ops.device)
-        recv = self._buf("recv", self.world * S, ops.device)
+        if S == 0:
+            return
+        keys = ("send", "recv") if defer is None else (("dsend", depth), ("drecv", depth))
+        send = self._buf(keys[0], S, ops.device)
+        recv = self._buf(keys[1], self.world * S, ops.device)
         if sizes[self.rank]:
             ops.pack(*pieces[self.rank], send, False)
-        for r, p in enumerate(pieces):
-            if r != self.rank and sizes[r]:
-                ops.pack(*p, recv[r * S:r * S + sizes[r]], True)
+        entry = (defer, None, send, recv, None, pieces, sizes, S)
         self.exchanged += sum(sizes)
+        if defer is None:
+            self._unpack(entry)
+        else:
+            self._pending.append(entry)
 
 
 def main():
