@@ -333,8 +333,9 @@ struct Fact {
   double* tmp;       // n x NBI: out-of-place TRSM leaf output (or null)
   double* diag_out;  // [n] or null
   int* info;
-  double* part;      // split-K partials, PART_ELEMS doubles (or null)
+  double* part;      // split-K partials, part_elems doubles (or null)
   hipStream_t s;
+  int64_t part_elems = 0;
   int64_t diag_n = 0;  // batched: diag_out stride (the matrix order)
   // batched recursion: `batch` matrices at stride sA, each with its own copy of the workspace
   // (stride sW doubles from ws0); a pointer into [ws0, ws0 + sW) is a workspace operand
@@ -352,9 +353,17 @@ struct Fact {
   }
 };
 
-// Split-K partials for the recursion's few-tile GEMMs (the 128..1024 levels: a 128^3 TRSM or SYRK
-// is one 128x128 tile, i.e. one CU): up to 8 splits, bounded by this many doubles (16 MB).
-constexpr int64_t PART_ELEMS = 2 << 20;
+// Split-K partials for the recursion's few-tile GEMMs (the 128..2048 levels: a 128^3 TRSM or SYRK
+// is one 128x128 tile, i.e. one CU): up to 8 splits, bounded by the partials area.  One matrix:
+// 64 MB.  At 16 MB the 2048-level SYRKs and TRSMs (136..256 tiles, K = 512..2048) ran unsplit on
+// half the CUs or less; 64 MB splits them: the 65k step 0.3 % faster on one GPU, and each rank's
+// factor share at R = 8 6 % faster (those levels are replicated on every rank;
+// profiles/r6_splitk_part_ab.json, profiles/r6_sharded_step_part_ab.json).  Batched
+// factorizations (the VGP step's M x M matrices, the multifrontal fronts) keep 16 MB per matrix:
+// their products are at most 1024 wide, and the larger per-matrix workspace stride cost the C3
+// step 0.05 ms (profiles/r6_vgp_part_ab.txt).
+constexpr int64_t PART_ELEMS = 8 << 20;
+constexpr int64_t PART_ELEMS_BATCHED = 2 << 20;
 
 // C = alpha op(A) op(B) + beta C with the split count of vgposp_gemm_splitk, reduced to what the
 // partials area holds.  In-place operands (C also read as A) are safe: the split kernels only
@@ -363,7 +372,7 @@ static int pgemm(const Fact& f, int transa, int transb, int64_t m, int64_t n, in
                  double alpha, const double* A, int64_t lda, const double* B, int64_t ldb,
                  double beta, double* C, int64_t ldc, int uplo_c, int tri_a, int tri_b) {
   int sp = f.part ? gemm_auto_splits(m, n, k, uplo_c, transa) : 1;
-  while (sp > 1 && (int64_t)sp * m * n > PART_ELEMS) --sp;
+  while (sp > 1 && (int64_t)sp * m * n > f.part_elems) --sp;
   if (f.batch > 1)
     return gemm_launch_batched(transa, transb, m, n, k, alpha, A, lda, f.stride(A), B, ldb,
                                f.stride(B), beta, C, ldc, f.stride(C), uplo_c, tri_a, tri_b, sp,
@@ -567,17 +576,21 @@ static Fact make_fact(int64_t n, int64_t lda, void* ws, double* diag_out, int* i
   double* xinv = blocks ? work + n1 * (n - n1) : nullptr;
   double* tmp = blocks ? xinv + n * NBI : nullptr;
   double* part = n > NB ? work + n1 * (n - n1) + (blocks ? 2 * n * NBI : 0) : nullptr;
-  return Fact{lda, base, work, xinv, tmp, diag_out, info, part, stream};
+  Fact f{lda, base, work, xinv, tmp, diag_out, info, part, stream};
+  f.part_elems = PART_ELEMS;
+  return f;
 }
 
 // `batch` matrices at stride sA factored by ONE recursion: every launch covers all of them (the
 // leaves as one workgroup per matrix, the GEMMs with a batch grid dimension), so B small
 // factorizations cost the launches and the latency chain of one.  ws holds B copies of the
 // single-matrix workspace.
-// Per-matrix workspace of a batched factorization without the split-K partials (large batches
-// fill the GPU through the batch dimension; 16 MB of partials per matrix would not fit).
+// Per-matrix workspace of a batched factorization: the single-matrix layout with a 16 MB partials
+// area (use_part) or none (large batches fill the GPU through the batch dimension; 16 MB of
+// partials per matrix would not fit).
 size_t potrf_ws_bytes_opt(int64_t n, bool use_part) {
-  return potrf_ws_bytes(n) - ((!use_part && n > NB) ? (size_t)PART_ELEMS * sizeof(double) : 0);
+  const int64_t part = n > NB ? (use_part ? PART_ELEMS_BATCHED : 0) : 0;
+  return potrf_ws_bytes(n) - (size_t)((n > NB ? PART_ELEMS : 0) - part) * sizeof(double);
 }
 
 int potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int batch, int invert,
@@ -596,6 +609,7 @@ int potrf_batched(double* A, int64_t n, int64_t lda, int64_t sA, int batch, int 
   const bool blocks = n > NBI;
   Fact f = make_fact(n, lda, ws, diag_out, info, stream);
   if (!use_part) f.part = nullptr;
+  f.part_elems = PART_ELEMS_BATCHED;
   f.batch = batch;
   f.sA = sA;
   f.sW = (int64_t)(potrf_ws_bytes_opt(n, use_part) / sizeof(double));
@@ -768,7 +782,7 @@ static int trsm_left_rec(const Fact& f, const double* Lp, int64_t ldl, int64_t n
 
 size_t trsm_ws_bytes(int64_t n, int64_t m) {
   const int64_t leaves = (n + NB - 1) / NB;
-  return (size_t)(leaves * NB * NB + NB * m + PART_ELEMS + 64) * sizeof(double);
+  return (size_t)(leaves * NB * NB + NB * m + PART_ELEMS_BATCHED + 64) * sizeof(double);
 }
 
 int trsm_left(const double* L, int64_t n, int64_t ldl, int trans, double* B, int64_t m,
@@ -778,7 +792,7 @@ int trsm_left(const double* L, int64_t n, int64_t ldl, int trans, double* B, int
   const int64_t nl = (n + NB - 1) / NB, nfull = n / NB;
   double* tmp = leaves + nl * NB * NB;
   double* part = tmp + NB * m;
-  int* dummy = reinterpret_cast<int*>(part + PART_ELEMS);  // the invert-only leaves never write it
+  int* dummy = reinterpret_cast<int*>(part + PART_ELEMS_BATCHED);  // the invert-only leaves never write it
   {
     ProfScope ps("trtri_leaf", s, 0.0, 8.0 * NB * NB * 2 * nl);
     if (nfull > 0)
@@ -793,6 +807,7 @@ int trsm_left(const double* L, int64_t n, int64_t ldl, int trans, double* B, int
     VG_LAUNCH_CHECK();
   }
   Fact f{ldl, leaves, nullptr, nullptr, tmp, nullptr, dummy, part, s};
+  f.part_elems = PART_ELEMS_BATCHED;  // the TRSM's products are at most n x m: 16 MB as before
   return trsm_left_rec(f, L, ldl, n, 0, trans, B, m, ldb);
 }
 
