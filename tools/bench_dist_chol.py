@@ -40,6 +40,7 @@ class LocalDist(DistCholesky):
             ops.pack(*pieces[self.rank], send, False)
         entry = (defer, None, send, recv, None, pieces, sizes, S)
         self.exchanged += sum(sizes)
+        self.n_exchanges = getattr(self, "n_exchanges", 0) + 1
         if defer is None:
             self._unpack(entry)
         else:

@@ -32,6 +32,8 @@ from vgposp_amd.workloads import placement_split  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", nargs="+", type=int, default=[1, 2, 4, 8])
+    ap.add_argument("--dist-min", type=int, default=DIST_MIN,
+                    help="smallest node whose panel / SYRK are split over the ranks")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r6_sharded_step_per_rank.json"))
     a = ap.parse_args()
     with open(os.path.join(ROOT, "tests", "golden", "bench65k_cpu_picks.json")) as f:
@@ -66,7 +68,7 @@ def main():
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    out = {"N": N, "k": k, "dist_min": DIST_MIN, "per_R": {}}
+    out = {"N": N, "k": k, "dist_min": a.dist_min, "per_R": {}}
     for R in a.ranks:
         ranks = []
         slabs = inverse_slabs(N, R)
@@ -79,10 +81,11 @@ def main():
                 rec["exchanged_GB"] = 0.0
             else:
                 b.prepare()
-                dc = LocalDist(b.chol_ops(), r, R, DIST_MIN)
+                dc = LocalDist(b.chol_ops(), r, R, a.dist_min)
                 rec["factor_s"] = timed(dc.factor)
                 rec["inverse_slab_s"] = timed(lambda: b.finish_slab(c0, c1))
                 rec["exchanged_GB"] = 8 * dc.exchanged / 1e9
+                rec["all_gathers"] = getattr(dc, "n_exchanges", 0)
             rec["rounds_s"] = timed(lambda: rounds(c0, c1, R > 1))
             rec["total_s"] = sum(v for kk, v in rec.items() if kk.endswith("_s"))
             ranks.append(rec)
